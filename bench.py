@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""bench.py -- GP fit + posterior on MI355X through libgpr_hip.so (BASELINE.json metric).
+
+Workload (BASELINE config 3, the config the headline metric is quoted on): composed kernel
+SquaredExp + SquaredExp + WhiteNoise (the parity-pinned stand-in for "SE + periodic": the
+reference has no periodic kernel), N = 32768 training points, d = 8, fp64.
+One step = one GP job on each GPU:
+    fit      : K-assembly (N x N) + in-place blocked POTRF + POTRS (alpha = K^{-1} y)
+    posterior: cross kernel (N x np) + mean + diagonal variance for np = 8192 test points
+Synthetic data: x ~ U[0,1)^(d x N) seed 0 (+rank), y = sin(sum x)^2, test points
+seed 1 (+rank); hp sigma = 1, l = 3 sqrt(8/d), sigma_n = 0.1.  All inputs are resident in
+HBM before the timed region.
+
+Multi-GPU: the fit does not shard (no distributed Cholesky) -- every rank runs its
+own job ("replicas", weak scaling, no data-path collective); value = jobs/s over all ranks.
+
+Extra fields: K-build GB/s (8 N^2 / t) and POTRF TFLOP/s ((N^3/3) / t) at N = 32768, stage
+times, and `roofline` for the dominant kernel (gemm_tn_kernel, the FP64 MFMA GEMM that runs
+every POTRF trailing update / panel and the posterior TRSM) measured with HIP events on the
+context stream over one instrumented step; `cpu_baseline` = the CPU oracle (threaded C
+K-build + OpenBLAS LAPACK) on a bounded sample (N = 8192, np = 2048), scaled to the job.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gaussianprocessregression.jl_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_MFMA_PEAK = 78.6      # TFLOP/s, FP64 matrix spec (measured 77.5 in tools/probe)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=32768)
+    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--np", type=int, default=8192, dest="npred")
+    ap.add_argument("--kernel", default="SE+SE+WN")
+    ap.add_argument("--nb", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-n", type=int, default=8192)
+    ap.add_argument("--cpu-np", type=int, default=2048)
+    return ap.parse_args()
+
+
+def kinds_of(name):
+    return [1 if k == "SE" else 2 for k in name.split("+")]
+
+
+def default_hp(kinds, d, noise=0.1):
+    hp = []
+    for k in kinds:
+        hp += [1.0] + [3.0 * math.sqrt(8.0 / d)] * d if k == 1 else [noise]
+    return np.array(hp, dtype=np.float64)
+
+
+def cpu_baseline(a, kinds, hp):
+    """Time the CPU oracle (test infrastructure, bench's cpu_baseline leg only) on a bounded
+    sample and scale each stage to the full job by its complexity."""
+    import scipy.linalg as sla
+
+    from oracle import gpr_oracle as O
+    from oracle.cpu_kbuild import kbuild_cpu
+
+    n, m, d = a.cpu_n, a.cpu_np, a.d
+    x = np.random.default_rng(0).random((d, n))
+    y = np.sin(x.sum(0)) ** 2
+    xp = np.random.default_rng(1).random((d, m))
+    okinds = [O.SE if k == 1 else O.WN for k in kinds]
+    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+
+    def run():
+        t0 = time.perf_counter()
+        K = kbuild_cpu(okinds, hp, x)
+        t1 = time.perf_counter()
+        U = sla.cholesky(K, lower=False, overwrite_a=True, check_finite=False)
+        t2 = time.perf_counter()
+        alpha = O.cho_solve_upper(U, y)
+        t3 = time.perf_counter()
+        Kpx = kbuild_cpu(okinds, hp, x, xp)
+        mu = Kpx.T @ alpha
+        V = sla.solve_triangular(U, Kpx, trans="T", lower=False, check_finite=False,
+                                 overwrite_b=True)
+        var = O.diag_prior(okinds, hp, d) - np.einsum("ij,ij->j", V, V)
+        t4 = time.perf_counter()
+        assert np.isfinite(mu).all() and np.isfinite(var).all()
+        return np.array([t1 - t0, t2 - t1, t3 - t2, t4 - t3])
+
+    run()  # warm-up
+    reps = [run() for _ in range(3)]
+    t = np.median(np.stack(reps), axis=0)
+    N, NP = a.n, a.npred
+    scale = np.array([(N / n) ** 2, (N / n) ** 3, (N / n) ** 2, (NP / m) * (N / n) ** 2])
+    t_job = float(np.sum(t * scale))
+    return {
+        "value": 1.0 / t_job,
+        "unit": "GP jobs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle (C OpenMP K-build + OpenBLAS dpotrf/dtrsm via SciPy) at N={n}, "
+                   f"np={m}, median of 3 after 1 warm-up: stages [kbuild, potrf, potrs, "
+                   f"posterior] = {[round(v, 4) for v in t.tolist()]} s, scaled to N={N}, "
+                   f"np={NP} by N^2 / N^3 / N^2 / np*N^2 -> {t_job:.2f} s per job"),
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import gpr_amd as G
+    from gpr_amd import _lib
+
+    lib = _lib.lib
+    ctx = G.Context(local, nb=a.nb)
+    N, d, NP = a.n, a.d, a.npred
+    kinds = kinds_of(a.kernel)
+    hp = default_hp(kinds, d)
+    karr = (ctypes.c_int * len(kinds))(*kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+    x = np.random.default_rng(0 + rank).random((d, N))
+    y = np.sin(x.sum(0)) ** 2
+    xp = np.random.default_rng(1 + rank).random((d, NP))
+    dx, dy, dxp = ctx.colmajor(x), ctx.colmajor(y), ctx.colmajor(xp)
+    K = ctx.empty(N, N)
+    alpha = ctx.empty(N)
+    mu = ctx.empty(NP)
+    var = ctx.empty(NP)
+    work = ctx.empty(NP, N)
+    info = ctypes.c_int(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def fit():
+        rc = lib.gpr_fit(ctx.h, karr, len(kinds), hpp, d, P(dx), N, P(dy), 1, N, 1e-8, P(K), N,
+                         P(alpha), ctypes.byref(info))
+        if rc != 0:
+            raise RuntimeError(f"gpr_fit rc={rc} info={info.value}: {lib.gpr_last_error(ctx.h)}")
+
+    def posterior():
+        ctx.check(lib.gpr_predict(ctx.h, karr, len(kinds), hpp, d, P(dx), N, P(K), N, P(alpha), 1,
+                                  P(dxp), NP, 1, 1e-8, P(mu), P(var), NP, P(work)), "gpr_predict")
+
+    def step():
+        fit()
+        posterior()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    ctx.sync()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    dt = (t1 - t0) / a.steps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ok = bool(torch.isfinite(mu).all().item() and torch.isfinite(var).all().item())
+
+    # ---- instrumented step (HIP events on the context stream) --------------------------
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    stg = {}
+    with torch.cuda.stream(ctx.stream):
+        lib.gpr_timing_reset(ctx.h)
+        lib.gpr_timing_enable(ctx.h, 1)
+        e = [ev() for _ in range(5)]
+        e[0].record(ctx.stream)
+        kinds_k = (ctypes.c_int * len(kinds))(*kinds)
+        ctx.check(lib.gpr_kernel(ctx.h, kinds_k, len(kinds), hpp, d, P(dx), N, None, N, 1, 1e-8,
+                                 P(K), N), "gpr_kernel")
+        e[1].record(ctx.stream)
+        ctx.check(lib.gpr_potrf_upper(ctx.h, P(K), N, N, ctypes.byref(info)), "potrf")
+        e[2].record(ctx.stream)
+        alpha.copy_(dy)
+        ctx.check(lib.gpr_potrs_upper(ctx.h, P(K), N, N, P(alpha), 1, N), "potrs")
+        e[3].record(ctx.stream)
+        posterior()
+        e[4].record(ctx.stream)
+        ctx.sync()
+        lib.gpr_timing_enable(ctx.h, 0)
+    names = ["kbuild", "potrf", "potrs", "posterior"]
+    for i, nm in enumerate(names):
+        stg[nm] = e[i].elapsed_time(e[i + 1])
+    cls = {}
+    for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other"]):
+        ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        lib.gpr_timing_get(ctx.h, c, ctypes.byref(ms), ctypes.byref(ln), ctypes.byref(fl))
+        cls[nm] = (ms.value, ln.value, fl.value)
+    kb_ms = cls["kbuild"][0]
+    kbuild_gbs = 8.0 * N * N / (kb_ms * 1e-3) / 1e9
+    potrf_tf = (N ** 3 / 3.0) / (stg["potrf"] * 1e-3) / 1e12
+    # dominant kernel: gemm_tn_kernel = classes syrk + panel GEMMs + trsm_gemm (+ others not
+    # counted); timed per launch.  Panel class also holds the diag kernels (flops 0).
+    g_ms = cls["syrk"][0] + cls["trsm_gemm"][0]
+    g_launch = cls["syrk"][1] + cls["trsm_gemm"][1]
+    g_fl = cls["syrk"][2] + cls["trsm_gemm"][2]
+    achieved = g_fl / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "GP-fit+predict wall-time and K-build GB/s + POTRF TFLOP/s at N=32768",
+            "value": world / dt,
+            "unit": "GP jobs/s (fit N=%d + posterior mean/var np=%d, per GPU)" % (N, NP),
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (x~U[0,1)^(d x N) seeded, y=sin(sum x)^2)",
+            "config": {"workload": f"C3 fit+posterior: {a.kernel}, N={N}, d={d}, np={NP}",
+                       "N": N, "d": d, "np": NP, "kernel": a.kernel, "nb": a.nb,
+                       "parallelism": f"replicas x{world}"},
+            "kbuild_GBps": kbuild_gbs,
+            "kbuild_hbm_frac": kbuild_gbs / HBM_PEAK_GBS,
+            "potrf_TFLOPs": potrf_tf,
+            "potrf_mfma_frac": potrf_tf / FP64_MFMA_PEAK,
+            "stage_ms": stg,
+            "syrk_TFLOPs": cls["syrk"][2] / (cls["syrk"][0] * 1e-3) / 1e12 if cls["syrk"][0] else None,
+            "roofline": {
+                "kernel": "gemm_tn_kernel (POTRF trailing SYRK + posterior TRSM GEMMs)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP64_MFMA_PEAK,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK,
+                "traffic": None,
+                "launches": g_launch,
+                "avg_launch_us": g_ms * 1e3 / max(g_launch, 1),
+                "flops_per_launch": g_fl / max(g_launch, 1),
+            },
+            "results_finite": ok,
+        }
+        if not a.no_cpu_baseline and world == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline(a, kinds, hp)
+            except Exception as ex:  # never let the baseline leg kill the bench line
+                out["cpu_baseline"] = {"value": None, "error": repr(ex)}
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

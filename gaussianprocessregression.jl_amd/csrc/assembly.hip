@@ -1,0 +1,427 @@
+// Kernel-matrix assembly on gfx950: SquaredExp / composed K, cross K, dK/dtheta.
+//
+// Reference: kernel_impl!(::SquaredExp) src/covariance.jl:85-95 (scale x by l, squared
+// Euclidean distance src/covariance.jl:72-77, sigma^2 exp(-D)), the +eps jitter rule
+// src/covariance.jl:49-58, the composed sum/noise src/compose_covar.jl:47-77 and the GPU
+// broadcast seam src/covar_gpu.jl:1-18 this replaces.
+//
+// Design (HBM-write bound): the inputs are pre-scaled once per SE part (xs = x .* l, the
+// reference's own rounding order) into a tiny workspace; a 64x64 output tile per 256-thread
+// workgroup keeps the row point's d features in registers and reads the column point's
+// features with scalar (wave-uniform) loads.  For the symmetric K only upper tiles are
+// computed; each is stored directly and, transposed through LDS, as its mirror tile, so
+// every N^2 element is written exactly once with 512-B coalesced column segments and the
+// exp work is halved.
+#include "common.hpp"
+
+namespace {
+
+constexpr int KT = 64;  // output tile edge
+
+// xs[p][k + a*d] = x[k + a*d] * l_p[k]   (x .* ls[:, n], src/covariance.jl:90)
+__global__ void scale_inputs_kernel(KParams kp, const double* __restrict__ X, int n,
+                                    double* __restrict__ xs) {
+  const int d = kp.d;
+  const size_t total = (size_t)n * d;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total * kp.nse;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int p = (int)(t / total);
+    const size_t r = t - p * total;
+    const int k = (int)(r % d);
+    xs[t] = X[r] * kp.l[p][k];
+  }
+}
+
+// D = sum_k (xr_k - xc_k)^2 with xr in registers and xc wave-uniform (scalar loads).
+template <int D>
+__device__ __forceinline__ double sqdist(const double* xr, const double* __restrict__ xc,
+                                         int d) {
+  double s = 0.0;
+  if constexpr (D > 0) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const double t = xr[k] - xc[k];
+      s = fma(t, t, s);
+    }
+  } else {
+    for (int k = 0; k < d; ++k) {
+      const double t = xr[k] - xc[k];
+      s = fma(t, t, s);
+    }
+  }
+  return s;
+}
+
+// Symmetric K (same-object call): upper tiles (bi <= bj) + LDS-transposed mirror.
+template <int D>
+__global__ __launch_bounds__(256) void kmat_sym_kernel(KParams kp, const double* __restrict__ xs,
+                                                       int n, double* __restrict__ K,
+                                                       size_t ldk) {
+  __shared__ double tr[KT * (KT + 1)];
+  const int bid = blockIdx.x;
+  int bj = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+  while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
+  while (bj * (bj + 1) / 2 > bid) --bj;
+  const int bi = bid - bj * (bj + 1) / 2;
+  const int i0 = bi * KT, j0 = bj * KT;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int d = kp.d;
+  const int i = i0 + lane;
+  const bool irow = i < n;
+
+  double vals[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) vals[c] = 0.0;
+  // parts outermost so only one part's row features live in registers; the per-element
+  // accumulation order stays part 1, part 2, ... as in src/compose_covar.jl:52-56.
+  for (int p = 0; p < kp.nse; ++p) {
+    const double* xrow = xs + ((size_t)p * n + (irow ? i : 0)) * d;
+    double xr[D > 0 ? D : 1];
+    if constexpr (D > 0) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) xr[k] = xrow[k];
+    }
+    const double s2 = kp.sigma[p] * kp.sigma[p];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int j = j0 + wv + 4 * c;  // wave-uniform column
+      if (j < n) {
+        const double* xc = xs + ((size_t)p * n + j) * d;
+        double dist;
+        if constexpr (D > 0) {
+          dist = sqdist<D>(xr, xc, d);
+        } else {
+          dist = sqdist<0>(xrow, xc, d);
+        }
+        double t = s2 * exp(-1.0 * dist);
+        if (i == j) t += kp.eps;
+        vals[c] = (p == 0) ? t : vals[c] + t;
+      }
+    }
+  }
+  if (kp.has_noise) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (i == j0 + wv + 4 * c) vals[c] += kp.noise2;
+  }
+  // direct tile: K[i + j*ldk], lanes along i -> 512-B column segments
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int j = j0 + wv + 4 * c;
+    if (irow && j < n) K[(size_t)i + (size_t)j * ldk] = vals[c];
+  }
+  if (bi == bj) return;
+  // mirror tile through LDS: tr[jl][il]
+#pragma unroll
+  for (int c = 0; c < 16; ++c) tr[(wv + 4 * c) * (KT + 1) + lane] = vals[c];
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int il = wv + 4 * c;     // row of the original tile
+    const int jj = j0 + lane;      // mirrored row index
+    const int ii = i0 + il;        // mirrored column index
+    if (jj < n && ii < n) K[(size_t)jj + (size_t)ii * ldk] = tr[lane * (KT + 1) + il];
+  }
+}
+
+// Cross kernel K[n x m] (x !== xp): no eps, no noise.  Rows from xs (n), cols from xps (m).
+template <int D>
+__global__ __launch_bounds__(256) void kmat_cross_kernel(KParams kp, const double* __restrict__ xs,
+                                                         int n, const double* __restrict__ xps,
+                                                         int m, double* __restrict__ K,
+                                                         size_t ldk, int ntile_i) {
+  const int bi = blockIdx.x % ntile_i;
+  const int bj = blockIdx.x / ntile_i;
+  const int i0 = bi * KT, j0 = bj * KT;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int d = kp.d;
+  const int i = i0 + lane;
+  const bool irow = i < n;
+  double vals[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) vals[c] = 0.0;
+  for (int p = 0; p < kp.nse; ++p) {
+    const double* xrow = xs + ((size_t)p * n + (irow ? i : 0)) * d;
+    double xr[D > 0 ? D : 1];
+    if constexpr (D > 0) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) xr[k] = xrow[k];
+    }
+    const double s2 = kp.sigma[p] * kp.sigma[p];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int j = j0 + wv + 4 * c;
+      if (j < m) {
+        const double* xc = xps + ((size_t)p * m + j) * d;
+        double dist;
+        if constexpr (D > 0) {
+          dist = sqdist<D>(xr, xc, d);
+        } else {
+          dist = sqdist<0>(xrow, xc, d);
+        }
+        const double t = s2 * exp(-1.0 * dist);
+        vals[c] = (p == 0) ? t : vals[c] + t;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int j = j0 + wv + 4 * c;
+    if (irow && j < m) K[(size_t)i + (size_t)j * ldk] = vals[c];
+  }
+}
+
+// dK/dtheta for one hyper-parameter (src/deriv_covar.jl:20-29): part p of the composed
+// kernel, which = 0 -> (2/|sigma|) K_p (K_p incl. eps on the diagonal),
+// which = k+1 -> -2 l_k K_p (x_k,a - x_k,b)^2 with RAW x.
+__global__ void kgrad_kernel(KParams kp, const double* __restrict__ X,
+                             const double* __restrict__ xs, int n, int p, int which,
+                             double* __restrict__ DK, size_t ld) {
+  const int d = kp.d;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)n * n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int a = (int)(t % n), b = (int)(t / n);
+    const double* xa = xs + ((size_t)p * n + a) * d;
+    const double* xb = xs + ((size_t)p * n + b) * d;
+    double s = 0.0;
+    for (int k = 0; k < d; ++k) {
+      const double q = xa[k] - xb[k];
+      s = fma(q, q, s);
+    }
+    double Kp = kp.sigma[p] * kp.sigma[p] * exp(-1.0 * s);
+    if (a == b) Kp += kp.eps;
+    double v;
+    if (which == 0) {
+      v = (2.0 / fabs(kp.sigma[p])) * Kp;
+    } else {
+      const int k = which - 1;
+      const double dx = X[(size_t)a * d + k] - X[(size_t)b * d + k];
+      v = -2.0 * kp.l[p][k] * Kp * (dx * dx);
+    }
+    DK[(size_t)a + (size_t)b * ld] = v;
+  }
+}
+
+__global__ void diag_scaled_identity_kernel(double* __restrict__ A, int n, size_t lda,
+                                            double lam) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)n * n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int a = (int)(t % n), b = (int)(t / n);
+    A[(size_t)a + (size_t)b * lda] = (a == b) ? lam : 0.0;
+  }
+}
+
+// lower <- upper^T, in 64x64 tiles through LDS (coalesced both ways)
+__global__ __launch_bounds__(256) void mirror_upper_kernel(double* __restrict__ A, int n,
+                                                           size_t lda) {
+  __shared__ double tr[KT * (KT + 1)];
+  const int bid = blockIdx.x;
+  int bj = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+  while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
+  while (bj * (bj + 1) / 2 > bid) --bj;
+  const int bi = bid - bj * (bj + 1) / 2;  // bi <= bj: source tile (rows bi, cols bj)
+  const int i0 = bi * KT, j0 = bj * KT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int c = 0; c < 16; ++c) {
+    const int j = j0 + wv + 4 * c, i = i0 + lane;
+    tr[(wv + 4 * c) * (KT + 1) + lane] = (i < n && j < n) ? A[(size_t)i + (size_t)j * lda] : 0.0;
+  }
+  __syncthreads();
+  for (int c = 0; c < 16; ++c) {
+    const int il = wv + 4 * c;
+    const int jj = j0 + lane, ii = i0 + il;  // destination (jj, ii), jj >= ii region
+    if (jj < n && ii < n && jj > ii) A[(size_t)jj + (size_t)ii * lda] = tr[lane * (KT + 1) + il];
+  }
+}
+
+__global__ void set_identity_kernel(double* __restrict__ A, int n, size_t lda) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)n * n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int a = (int)(t % n), b = (int)(t / n);
+    A[(size_t)a + (size_t)b * lda] = (a == b) ? 1.0 : 0.0;
+  }
+}
+
+int scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, double** buf,
+                 size_t* cap) {
+  GPR_TRY(ensure_buf(ctx, buf, cap, (size_t)kp.nse * kp.d * n + 1));
+  const size_t total = (size_t)kp.nse * kp.d * n;
+  int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  if (blocks < 1) blocks = 1;
+  scale_inputs_kernel<<<blocks, 256, 0, ctx->stream>>>(kp, dX, n, *buf);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+template <int D>
+void launch_sym(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk) {
+  const int nt = (n + KT - 1) / KT;
+  const long long nblk = (long long)nt * (nt + 1) / 2;
+  kmat_sym_kernel<D><<<(unsigned)nblk, 256, 0, ctx->stream>>>(kp, xs, n, K, (size_t)ldk);
+}
+
+template <int D>
+void launch_cross(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const double* xps,
+                  int m, double* K, int ldk) {
+  const int nti = (n + KT - 1) / KT, ntj = (m + KT - 1) / KT;
+  kmat_cross_kernel<D><<<(unsigned)((long long)nti * ntj), 256, 0, ctx->stream>>>(
+      kp, xs, n, xps, m, K, (size_t)ldk, nti);
+}
+
+#define DISPATCH_D(FN, ...)                 \
+  switch (kp.d) {                           \
+    case 1: FN<1>(__VA_ARGS__); break;      \
+    case 2: FN<2>(__VA_ARGS__); break;      \
+    case 3: FN<3>(__VA_ARGS__); break;      \
+    case 4: FN<4>(__VA_ARGS__); break;      \
+    case 5: FN<5>(__VA_ARGS__); break;      \
+    case 6: FN<6>(__VA_ARGS__); break;      \
+    case 7: FN<7>(__VA_ARGS__); break;      \
+    case 8: FN<8>(__VA_ARGS__); break;      \
+    case 16: FN<16>(__VA_ARGS__); break;    \
+    default: FN<0>(__VA_ARGS__); break;     \
+  }
+
+// Pairwise split-factor kernel (src/split_kernel.jl:108-159) on pre-scaled points.
+//   mode 0: Euclidean      v = s2 * exp(-sum (a-b)^2)
+//   mode 1: SplitDistanceA v = s2 * exp(-sum (b^2 + 2 a b))      (a = xe, b = xq)
+//   mode 2: SplitDistanceC v = s2 * exp(-sum (-2 a b))            (a = xs, b = xq)
+// out[ia*sa + ib*sb]; lanes run along whichever of a/b has unit stride.
+__global__ __launch_bounds__(256) void pair_kernel(int mode, int d, const double* __restrict__ xa,
+                                                   int na, const double* __restrict__ xb, int nb,
+                                                   double s2, double* __restrict__ out, size_t sa,
+                                                   size_t sb, int a_fast) {
+  const size_t total = (size_t)na * nb;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    int ia, ib;
+    if (a_fast) {
+      ia = (int)(t % na);
+      ib = (int)(t / na);
+    } else {
+      ib = (int)(t % nb);
+      ia = (int)(t / nb);
+    }
+    const double* pa = xa + (size_t)ia * d;
+    const double* pb = xb + (size_t)ib * d;
+    double D = 0.0;
+    if (mode == 0) {
+      for (int k = 0; k < d; ++k) {
+        const double q = pa[k] - pb[k];
+        D = fma(q, q, D);
+      }
+    } else if (mode == 1) {
+      for (int k = 0; k < d; ++k) D += pb[k] * pb[k] + 2.0 * pa[k] * pb[k];
+    } else {
+      for (int k = 0; k < d; ++k) D += -2.0 * pa[k] * pb[k];
+    }
+    out[(size_t)ia * sa + (size_t)ib * sb] = s2 * exp(-1.0 * D);
+  }
+}
+
+}  // namespace
+
+int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
+                         const double* dXp, int m, int same, double* dK, int ldk) {
+  if (n <= 0 || (!same && m <= 0)) return 0;
+  GPR_TRY(scale_inputs(ctx, kp, dX, n, &ctx->dxs, &ctx->xs_cap));
+  if (same) {
+    const double el = (double)n * n;
+    TimerScope ts(ctx, TC_KBUILD, el * 8.0);  // "flops" slot carries algorithmic bytes
+    DISPATCH_D(launch_sym, ctx, kp, ctx->dxs, n, dK, ldk);
+    LAUNCH_CHECK(ctx);
+  } else {
+    GPR_TRY(scale_inputs(ctx, kp, dXp, m, &ctx->dxps, &ctx->xps_cap));
+    TimerScope ts(ctx, TC_OTHER, 0.0);
+    DISPATCH_D(launch_cross, ctx, kp, ctx->dxs, n, ctx->dxps, m, dK, ldk);
+    LAUNCH_CHECK(ctx);
+  }
+  return 0;
+}
+
+int launch_scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, double* out) {
+  const size_t total = (size_t)kp.nse * kp.d * n;
+  if (total == 0) return 0;
+  int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+  scale_inputs_kernel<<<blocks, 256, 0, ctx->stream>>>(kp, dX, n, out);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int launch_pair(gpr_ctx* ctx, int mode, int d, const double* xa, int na, const double* xb, int nb,
+                double s2, double* out, size_t sa, size_t sb) {
+  if (na <= 0 || nb <= 0) return 0;
+  const size_t total = (size_t)na * nb;
+  int blocks = (int)std::min<size_t>((total + 255) / 256, 65536);
+  pair_kernel<<<blocks, 256, 0, ctx->stream>>>(mode, d, xa, na, xb, nb, s2, out, sa, sb,
+                                               sa == 1 ? 1 : 0);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int launch_mirror_upper(gpr_ctx* ctx, double* A, int n, int lda) {
+  if (n <= 1) return 0;
+  const int nt = (n + KT - 1) / KT;
+  const long long nblk = (long long)nt * (nt + 1) / 2;
+  mirror_upper_kernel<<<(unsigned)nblk, 256, 0, ctx->stream>>>(A, n, (size_t)lda);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int launch_set_identity(gpr_ctx* ctx, double* A, int n, int lda) {
+  int blocks = (int)std::min<long long>(((long long)n * n + 255) / 256, 8192);
+  set_identity_kernel<<<blocks, 256, 0, ctx->stream>>>(A, n, (size_t)lda);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+extern "C" {
+
+int gpr_kernel(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+               const double* dX, int n, const double* dXp, int m, int same, double eps,
+               double* dK, int ldk) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (!dX || !dK) return set_err(ctx, GPR_E_ARG, "NULL device pointer");
+  if (n < 0) return set_err(ctx, GPR_E_ARG, "n < 0");
+  if (same) m = n;
+  else if (!dXp) return set_err(ctx, GPR_E_ARG, "dXp is NULL for a cross kernel");
+  if (ldk < (n > 1 ? n : 1)) return set_err(ctx, GPR_E_ARG, "ldk=%d < n=%d", ldk, n);
+  return launch_kernel_matrix(ctx, kp, dX, n, dXp, m, same, dK, ldk);
+}
+
+int gpr_kernel_grad(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                    const double* dX, int n, int i, double eps, double* dDK, int ld) {
+  KParams kp;
+  int D = 0;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, &D));
+  if (i < 1 || i > D) return set_err(ctx, GPR_E_ARG, "hp index %d out of 1..%d", i, D);
+  if (ld < n) return set_err(ctx, GPR_E_ARG, "ld < n");
+  // find_idx (src/compose_covar.jl:109-115)
+  int off = 0, se = 0;
+  for (int t = 0; t < nk; ++t) {
+    const int w = kinds[t] == GPR_SE ? d + 1 : 1;
+    if (i - 1 < off + w) {
+      const int local = i - 1 - off;
+      const int blocks = (int)std::min<long long>(((long long)n * n + 255) / 256, 8192);
+      if (kinds[t] == GPR_WN) {  // grad(::WhiteNoise) = 2 sigma_n I  (src/deriv_covar.jl:31)
+        diag_scaled_identity_kernel<<<blocks, 256, 0, ctx->stream>>>(dDK, n, (size_t)ld,
+                                                                    2.0 * hp[off]);
+        LAUNCH_CHECK(ctx);
+        return 0;
+      }
+      GPR_TRY(scale_inputs(ctx, kp, dX, n, &ctx->dxs, &ctx->xs_cap));
+      kgrad_kernel<<<blocks, 256, 0, ctx->stream>>>(kp, dX, ctx->dxs, n, se, local, dDK,
+                                                    (size_t)ld);
+      LAUNCH_CHECK(ctx);
+      return 0;
+    }
+    off += w;
+    if (kinds[t] == GPR_SE) ++se;
+  }
+  return set_err(ctx, GPR_E_ARG, "hp index not found");
+}
+
+}  // extern "C"

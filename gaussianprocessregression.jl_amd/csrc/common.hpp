@@ -1,0 +1,139 @@
+// Shared internals of libgpr_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/gpr_hip.h"
+
+#define KMAXP 4   // max SquaredExp parts handled by the fused kernels
+#define KMAXD GPR_MAX_DIM
+
+// Kernel description passed BY VALUE to every assembly kernel (< 4 KB of kernargs).
+// Mirrors split(hp, dims) of src/compose_covar.jl:21-28: the SE parts in `+` order
+// and the first WhiteNoise part (add_noise! src/compose_covar.jl:63-71).
+struct KParams {
+  int d;          // input dimension
+  int nse;        // number of SquaredExp parts (1..KMAXP)
+  int has_noise;  // a WhiteNoise part is present
+  int hp_off_noise;              // flat hp index of sigma_n (for the gradient)
+  double eps;                    // jitter per SE part on a same-object diagonal
+  double noise2;                 // sigma_n^2
+  double noise_sigma;            // sigma_n
+  double sigma[KMAXP];           // sigma of each SE part
+  int hp_off[KMAXP];             // flat hp index of each SE part's sigma
+  double l[KMAXP][KMAXD];        // inverse length-scales (multipliers) per SE part
+};
+
+enum TimingClass { TC_KBUILD = 0, TC_SYRK = 1, TC_PANEL = 2, TC_TRSM_GEMM = 3, TC_OTHER = 4, TC_N = 5 };
+
+struct TimedLaunch {
+  int cls;
+  hipEvent_t a, b;
+  double flops;
+};
+
+struct gpr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  int nb = 128;  // panel width of the blocked factorisations
+
+  // cached inverses of the diagonal blocks of the last factor: winv[b] = U_bb^{-1}
+  // (nb x nb, column-major, strictly-lower part zero), one slot per block.
+  double* winv = nullptr;
+  size_t winv_cap = 0;  // doubles
+  const double* fac_ptr = nullptr;
+  int fac_n = 0, fac_ld = 0, fac_nb = 0;
+  bool fac_valid = false;
+
+  int* dinfo = nullptr;         // device info word
+  double* dscratch = nullptr;   // generic scratch (partials, small vectors)
+  size_t scratch_cap = 0;       // doubles
+  double* dbig = nullptr;       // large scratch (Z for potri, Kpx for predict, ...)
+  size_t big_cap = 0;           // doubles
+  double* dbig2 = nullptr;
+  size_t big2_cap = 0;
+  double* dxs = nullptr;        // per-part scaled training inputs  (nse x d x n)
+  size_t xs_cap = 0;
+  double* dxps = nullptr;       // per-part scaled second inputs    (nse x d x m)
+  size_t xps_cap = 0;
+
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> event_pool;
+  double t_ms[TC_N] = {0, 0, 0, 0, 0};
+  long long t_launches[TC_N] = {0, 0, 0, 0, 0};
+  double t_flops[TC_N] = {0, 0, 0, 0, 0};
+};
+
+// ---- error helpers -------------------------------------------------------------------
+int set_err(gpr_ctx* ctx, int code, const char* fmt, ...);
+
+#define HIP_TRY(ctx, expr)                                                          \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      return set_err(ctx, GPR_E_HIP, "%s failed: %s (%s:%d)", #expr,                \
+                     hipGetErrorString(_e), __FILE__, __LINE__);                    \
+  } while (0)
+
+#define GPR_TRY(expr)            \
+  do {                           \
+    int _r = (expr);             \
+    if (_r != 0) return _r;      \
+  } while (0)
+
+#define LAUNCH_CHECK(ctx) HIP_TRY(ctx, hipGetLastError())
+
+// ---- workspace ------------------------------------------------------------------------
+int ensure_buf(gpr_ctx* ctx, double** p, size_t* cap, size_t need_doubles);
+int ensure_winv(gpr_ctx* ctx, int n, int nb);
+
+// ---- timing ---------------------------------------------------------------------------
+struct TimerScope {
+  gpr_ctx* ctx;
+  TimedLaunch tl;
+  bool on;
+  TimerScope(gpr_ctx* c, int cls, double flops);
+  ~TimerScope();
+};
+
+// ---- parse a kernel description -------------------------------------------------------
+int make_kparams(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d,
+                 double eps, KParams* kp, int* D_total);
+
+// ---- cross-TU launchers ---------------------------------------------------------------
+// C[m,n] = alpha * sum_{k<K} P[k + m*ldp] * Q[k + n*ldq] (* qscale[k]) + beta * C[m,n]
+struct GemmArgs {
+  const double* P; int ldp;
+  const double* Q; int ldq;
+  double* C; int ldc;
+  int M, N, K;
+  double alpha, beta;
+  int upper;              // only tiles/elements with m <= n (SYRK upper)
+  int kfrom_n;            // tile's K loop starts at its n0 (triangular factor, Z^T Z)
+  int kmax_from_n;        // tile's K loop ends at min(K, n0+TN) (lower-triangular RHS)
+  const double* qscale;   // optional per-k scale of Q (diag(wt) C)
+  const double* E; int lde;  // optional Hadamard factor: C = beta*C + alpha*acc*E
+  double* norm_out;       // optional: norm_out[n] -= sum_m (result)^2 (needs M <= tile)
+  const int* info;        // optional: skip when *info != 0
+};
+int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class);
+
+int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
+                         const double* dXp, int m, int same, double* dK, int ldk);
+int launch_mirror_upper(gpr_ctx* ctx, double* A, int n, int lda);
+int launch_scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, double* out);
+int launch_pair(gpr_ctx* ctx, int mode, int d, const double* xa, int na, const double* xb, int nb,
+                double s2, double* out, size_t sa, size_t sb);
+int launch_set_identity(gpr_ctx* ctx, double* A, int n, int lda);
+int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info);
+int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);
+int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
+                 int ldb, double* norm_out, int lower_rhs);
+int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
+               int ldb);

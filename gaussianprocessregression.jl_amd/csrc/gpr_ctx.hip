@@ -1,0 +1,230 @@
+// Context, memory, error and timing plumbing of libgpr_hip.so.
+#include <cstdarg>
+#include <cstring>
+
+#include "common.hpp"
+
+int set_err(gpr_ctx* ctx, int code, const char* fmt, ...) {
+  if (ctx) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return code;
+}
+
+int ensure_buf(gpr_ctx* ctx, double** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return 0;
+  if (*p) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+  }
+  if (need == 0) need = 1;
+  if (hipMalloc((void**)p, need * sizeof(double)) != hipSuccess) {
+    *p = nullptr;
+    return set_err(ctx, GPR_E_NOMEM, "hipMalloc of %zu bytes failed", need * sizeof(double));
+  }
+  *cap = need;
+  return 0;
+}
+
+int ensure_winv(gpr_ctx* ctx, int n, int nb) {
+  size_t nblk = (size_t)((n + nb - 1) / nb);
+  return ensure_buf(ctx, &ctx->winv, &ctx->winv_cap, nblk * nb * nb);
+}
+
+// ---- timing ----------------------------------------------------------------------------
+static hipEvent_t get_event(gpr_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+TimerScope::TimerScope(gpr_ctx* c, int cls, double flops) : ctx(c), on(c->timing) {
+  if (!on) return;
+  tl.cls = cls;
+  tl.flops = flops;
+  tl.a = get_event(ctx);
+  tl.b = get_event(ctx);
+  hipEventRecord(tl.a, ctx->stream);
+}
+
+TimerScope::~TimerScope() {
+  if (!on) return;
+  hipEventRecord(tl.b, ctx->stream);
+  ctx->pending.push_back(tl);
+}
+
+static void drain_timing(gpr_ctx* ctx) {
+  if (ctx->pending.empty()) return;
+  hipStreamSynchronize(ctx->stream);
+  for (auto& t : ctx->pending) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, t.a, t.b);
+    ctx->t_ms[t.cls] += ms;
+    ctx->t_launches[t.cls] += 1;
+    ctx->t_flops[t.cls] += t.flops;
+    ctx->event_pool.push_back(t.a);
+    ctx->event_pool.push_back(t.b);
+  }
+  ctx->pending.clear();
+}
+
+// ---- kernel description ------------------------------------------------------------------
+int make_kparams(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d, double eps,
+                 KParams* kp, int* D_total) {
+  if (!kinds || nk <= 0 || nk > GPR_MAX_PARTS) return set_err(ctx, GPR_E_ARG, "bad kinds/nk (%d)", nk);
+  if (!hp) return set_err(ctx, GPR_E_ARG, "hp is NULL");
+  if (d <= 0 || d > KMAXD) return set_err(ctx, GPR_E_UNSUP, "d=%d unsupported (1..%d)", d, KMAXD);
+  memset(kp, 0, sizeof *kp);
+  kp->d = d;
+  kp->eps = eps;
+  int off = 0;
+  for (int i = 0; i < nk; ++i) {
+    if (kinds[i] == GPR_SE) {
+      if (kp->nse >= KMAXP) return set_err(ctx, GPR_E_UNSUP, "more than %d SquaredExp parts", KMAXP);
+      kp->sigma[kp->nse] = hp[off];
+      kp->hp_off[kp->nse] = off;
+      for (int k = 0; k < d; ++k) kp->l[kp->nse][k] = hp[off + 1 + k];
+      kp->nse++;
+      off += d + 1;
+    } else if (kinds[i] == GPR_WN) {
+      if (!kp->has_noise) {  // findfirst(WhiteNoise) -- src/compose_covar.jl:64-68
+        kp->has_noise = 1;
+        kp->noise_sigma = hp[off];
+        kp->noise2 = hp[off] * hp[off];
+        kp->hp_off_noise = off;
+      }
+      off += 1;
+    } else {
+      return set_err(ctx, GPR_E_ARG, "unknown kernel kind %d", kinds[i]);
+    }
+  }
+  if (kp->nse == 0) return set_err(ctx, GPR_E_ARG, "kernel needs at least one SquaredExp part");
+  if (D_total) *D_total = off;
+  return 0;
+}
+
+extern "C" {
+
+const char* gpr_version(void) { return "gpr_hip 0.1.0 (gfx950)"; }
+
+int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
+  if (!out) return GPR_E_ARG;
+  *out = nullptr;
+  gpr_ctx* ctx = new gpr_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete ctx;
+    return GPR_E_HIP;
+  }
+  if (stream) {
+    ctx->stream = (hipStream_t)stream;
+  } else {
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      return GPR_E_HIP;
+    }
+    ctx->own_stream = true;
+  }
+  if (hipMalloc((void**)&ctx->dinfo, 64) != hipSuccess) {
+    delete ctx;
+    return GPR_E_NOMEM;
+  }
+  *out = ctx;
+  return 0;
+}
+
+int gpr_ctx_destroy(gpr_ctx_t ctx) {
+  if (!ctx) return 0;
+  hipStreamSynchronize(ctx->stream);
+  drain_timing(ctx);
+  for (auto e : ctx->event_pool) hipEventDestroy(e);
+  if (ctx->winv) hipFree(ctx->winv);
+  if (ctx->dinfo) hipFree(ctx->dinfo);
+  if (ctx->dscratch) hipFree(ctx->dscratch);
+  if (ctx->dbig) hipFree(ctx->dbig);
+  if (ctx->dbig2) hipFree(ctx->dbig2);
+  if (ctx->dxs) hipFree(ctx->dxs);
+  if (ctx->dxps) hipFree(ctx->dxps);
+  if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return 0;
+}
+
+const char* gpr_last_error(gpr_ctx_t ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gpr_sync(gpr_ctx_t ctx) {
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+void* gpr_ctx_stream(gpr_ctx_t ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int gpr_malloc(gpr_ctx_t ctx, size_t bytes, void** dptr) {
+  if (!dptr) return set_err(ctx, GPR_E_ARG, "dptr is NULL");
+  if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess)
+    return set_err(ctx, GPR_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+  return 0;
+}
+
+int gpr_free(gpr_ctx_t ctx, void* dptr) {
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (dptr) HIP_TRY(ctx, hipFree(dptr));
+  return 0;
+}
+
+int gpr_upload(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes) {
+  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gpr_download(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes) {
+  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gpr_set_block(gpr_ctx_t ctx, int nb) {
+  if (nb != 64 && nb != 128) return set_err(ctx, GPR_E_ARG, "nb must be 64 or 128 (got %d)", nb);
+  ctx->nb = nb;
+  ctx->fac_valid = false;
+  return 0;
+}
+
+int gpr_timing_enable(gpr_ctx_t ctx, int on) {
+  ctx->timing = on != 0;
+  return 0;
+}
+
+int gpr_timing_get(gpr_ctx_t ctx, int cls, double* ms, long long* launches, double* flops) {
+  if (cls < 0 || cls >= TC_N) return set_err(ctx, GPR_E_ARG, "bad timing class %d", cls);
+  drain_timing(ctx);
+  if (ms) *ms = ctx->t_ms[cls];
+  if (launches) *launches = ctx->t_launches[cls];
+  if (flops) *flops = ctx->t_flops[cls];
+  return 0;
+}
+
+int gpr_timing_reset(gpr_ctx_t ctx) {
+  drain_timing(ctx);
+  for (int i = 0; i < TC_N; ++i) {
+    ctx->t_ms[i] = 0;
+    ctx->t_launches[i] = 0;
+    ctx->t_flops[i] = 0;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,255 @@
+// Fit, posterior and split-kernel block prediction on gfx950.
+//
+// gpr_fit      = update_cache!(MllLossCache / GPRPredictCache)  src/cost.jl:74-81,
+//                src/predict.jl:29-34
+// gpr_predict  = predict!/predict_mean!                         src/predict.jl:36-101
+// gpr_split_predict = kernel!(::SplitKernel) + split mean/var  src/split_kernel.jl:137-159,
+//                src/split_predict.jl:5-53
+//
+// Layout choice: the cross kernel is built TRANSPOSED w.r.t. the reference (Kpx = K(x, xp),
+// n x m, column j = test point j, contiguous over the training index), so that
+//   mu = Kpx^T wt               is a column-GEMV (coalesced), and
+//   V  = U^{-T} Kpx             is the same left-upper-transposed TRSM (MFMA GEMMs) as the
+//                               POTRF panels -- rdiv!(Kxp, U) of src/predict.jl:84 on Kxp^T,
+// with the diagonal variance ||V[:, j]||^2 accumulated in the TRSM's GEMM epilogue
+// (src/predict.jl:89-95 without a second pass over V).
+#include <cmath>
+
+#include "common.hpp"
+
+namespace {
+
+// y[j + c*ldy] = sum_i A[i + j*lda] x[i + c*ldx]: one wave per column j.
+__global__ __launch_bounds__(256) void colgemv_kernel(const double* __restrict__ A, size_t lda,
+                                                      int nrows, int ncols,
+                                                      const double* __restrict__ x, size_t ldx,
+                                                      int nrhs, double* __restrict__ y, size_t ldy) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= ncols) return;
+  const double* col = A + (size_t)j * lda;
+  for (int c = 0; c < nrhs; ++c) {
+    const double* xc = x + (size_t)c * ldx;
+    double s = 0.0;
+    for (int i = lane; i < nrows; i += 64) s = fma(col[i], xc[i], s);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) y[(size_t)j + (size_t)c * ldy] = s;
+  }
+}
+
+__global__ void fill_kernel(double* __restrict__ p, size_t n, double v) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x)
+    p[t] = v;
+}
+
+// KxqT[s + (jr*nq + q)*ns] = sum_p (A_p[el][q] * BT_p[s][el]) * C_p[s][q], el = e - e_lo.
+// Reference: Kxq .+= A[e,q] .* B[e,s] .* C[s,q]  (src/split_predict.jl:45-47), parts summed
+// from zero in order.
+__global__ __launch_bounds__(256) void split_kxq_kernel(int nse, const double* __restrict__ A,
+                                                        const double* __restrict__ BT,
+                                                        const double* __restrict__ C, int ns,
+                                                        int nq, int E_loc, int el0, int nrows,
+                                                        double* __restrict__ out) {
+  const size_t total = (size_t)ns * nq * nrows;
+  const size_t szA = (size_t)E_loc * nq, szB = (size_t)ns * E_loc, szC = (size_t)ns * nq;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int s = (int)(t % ns);
+    const size_t col = t / ns;
+    const int q = (int)(col % nq);
+    const int el = el0 + (int)(col / nq);
+    double v = 0.0;
+    for (int p = 0; p < nse; ++p) {
+      const double a = A[p * szA + (size_t)el + (size_t)q * E_loc];
+      const double b = BT[p * szB + (size_t)s + (size_t)el * ns];
+      const double c = C[p * szC + (size_t)s + (size_t)q * ns];
+      v += (a * b) * c;
+    }
+    out[t] = v;
+  }
+}
+
+int launch_fill(gpr_ctx* ctx, double* p, size_t n, double v) {
+  if (n == 0) return 0;
+  int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+  fill_kernel<<<blocks, 256, 0, ctx->stream>>>(p, n, v);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+// diagonal-variance prior: sigma^2 for a single SE (src/predict.jl:67); composed kernels:
+// sum over ALL parts of hp_part[1]^2, noise included (src/predict.jl:56-58).  No eps.
+double diag_prior(const int* kinds, int nk, const double* hp, int d) {
+  if (nk == 1) return hp[0] * hp[0];
+  double s = 0.0;
+  int off = 0;
+  for (int t = 0; t < nk; ++t) {
+    s += hp[off] * hp[off];
+    off += kinds[t] == GPR_SE ? d + 1 : 1;
+  }
+  return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, const double* dX,
+            int n, const double* dy, int nrhs, int ldy, double eps, double* dK, int ldk,
+            double* dalpha, int* info) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (n <= 0 || ldk < n || nrhs <= 0 || ldy < n || !dX || !dy || !dK || !dalpha)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  int hinfo = 0;
+  GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo));
+  if (info) *info = hinfo;
+  if (hinfo != 0) return hinfo;
+  HIP_TRY(ctx, hipMemcpy2DAsync(dalpha, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
+                                (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
+  GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
+  return 0;
+}
+
+int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, const double* dX,
+                int n, const double* dU, int ldu, const double* dwt, int nrhs, const double* dXp,
+                int m, int mode, double eps, double* dmu, double* dvar, int ldv, double* dwork) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (n <= 0 || m <= 0 || ldu < n || nrhs <= 0 || !dX || !dU || !dwt || !dXp || !dmu)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  if (mode != GPR_PREDICT_MEAN && !dvar) return set_err(ctx, GPR_E_ARG, "dvar is NULL");
+  if (mode == GPR_PREDICT_FULL && ldv < m) return set_err(ctx, GPR_E_ARG, "ldv < m");
+  double* Kpx = dwork;
+  if (!Kpx) {
+    GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)n * m));
+    Kpx = ctx->dbig2;
+  }
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, Kpx, n));  // K(x, xp), n x m
+  {
+    TimerScope ts(ctx, TC_OTHER, 0.0);
+    colgemv_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(Kpx, (size_t)n, n, m, dwt, (size_t)n, nrhs,
+                                                         dmu, (size_t)m);
+    LAUNCH_CHECK(ctx);
+  }
+  if (mode == GPR_PREDICT_MEAN) return 0;
+  if (mode == GPR_PREDICT_DIAG) {
+    GPR_TRY(launch_fill(ctx, dvar, (size_t)m, diag_prior(kinds, nk, hp, d)));
+    return trsm_ut_core(ctx, dU, n, ldu, Kpx, m, n, dvar, 0);
+  }
+  // full covariance: Sigma = K(xp, xp) (eps per SE part + noise) - V^T V
+  GPR_TRY(trsm_ut_core(ctx, dU, n, ldu, Kpx, m, n, nullptr, 0));
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dXp, m, nullptr, m, 1, dvar, ldv));
+  GemmArgs g{};
+  g.P = Kpx; g.ldp = n;
+  g.Q = Kpx; g.ldq = n;
+  g.C = dvar; g.ldc = ldv;
+  g.M = m; g.N = m; g.K = n;
+  g.alpha = -1.0; g.beta = 1.0;
+  g.upper = 1;
+  GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+  return launch_mirror_upper(ctx, dvar, m, ldv);
+}
+
+int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                      const double* dX, int ns, const double* dXe, int ne, const double* dXq,
+                      int nq, int part, double* dA, double* dB, double* dC) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, 0.0, &kp, nullptr));
+  if (part < 0 || part >= kp.nse) return set_err(ctx, GPR_E_ARG, "part out of range");
+  const size_t need = (size_t)kp.nse * d * (ns + ne + nq);
+  GPR_TRY(ensure_buf(ctx, &ctx->dxs, &ctx->xs_cap, need));
+  double* xs = ctx->dxs;
+  double* xes = xs + (size_t)kp.nse * d * ns;
+  double* xqs = xes + (size_t)kp.nse * d * ne;
+  GPR_TRY(launch_scale_inputs(ctx, kp, dX, ns, xs));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dXe, ne, xes));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dXq, nq, xqs));
+  const int p = part;
+  const double s2 = kp.sigma[p] * kp.sigma[p];
+  if (dA) GPR_TRY(launch_pair(ctx, 1, d, xes + (size_t)p * d * ne, ne, xqs + (size_t)p * d * nq, nq, 1.0, dA, 1, ne));
+  if (dB) GPR_TRY(launch_pair(ctx, 0, d, xes + (size_t)p * d * ne, ne, xs + (size_t)p * d * ns, ns, 1.0, dB, 1, ne));
+  if (dC) GPR_TRY(launch_pair(ctx, 2, d, xs + (size_t)p * d * ns, ns, xqs + (size_t)p * d * nq, nq, s2, dC, 1, ns));
+  return 0;
+}
+
+int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                      const double* dX, int ns, const double* dU, int ldu, const double* dwt,
+                      const double* dXe, int ne, const double* dXq, int nq, int e_lo, int e_hi,
+                      int var_lo, int var_hi, double eps, double* dmu, double* dvar) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (ns <= 0 || ne <= 0 || nq <= 0 || ldu < ns || !dX || !dU || !dwt || !dXe || !dXq || !dmu || !dvar)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  if (e_lo < 0 || e_hi > ne || e_lo > e_hi) return set_err(ctx, GPR_E_ARG, "bad e range [%d,%d)", e_lo, e_hi);
+  const int E = e_hi - e_lo;
+  if (E == 0) return 0;
+  const int nse = kp.nse;
+  // ---- factors for the local rows: A_p (E x nq), BT_p (ns x E), C_p (ns x nq)
+  const size_t szA = (size_t)E * nq, szB = (size_t)ns * E, szC = (size_t)ns * nq;
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)nse * (szA + szB + szC)));
+  double* A = ctx->dbig2;
+  double* BT = A + nse * szA;
+  double* C = BT + nse * szB;
+  const size_t nxs = (size_t)nse * d * (ns + E + nq);
+  GPR_TRY(ensure_buf(ctx, &ctx->dxs, &ctx->xs_cap, nxs));
+  double* xs = ctx->dxs;
+  double* xes = xs + (size_t)nse * d * ns;
+  double* xqs = xes + (size_t)nse * d * E;
+  {
+    TimerScope ts(ctx, TC_OTHER, 0.0);
+    GPR_TRY(launch_scale_inputs(ctx, kp, dX, ns, xs));
+    GPR_TRY(launch_scale_inputs(ctx, kp, dXe + (size_t)e_lo * d, E, xes));
+    GPR_TRY(launch_scale_inputs(ctx, kp, dXq, nq, xqs));
+    for (int p = 0; p < nse; ++p) {
+      const double s2 = kp.sigma[p] * kp.sigma[p];
+      // A: sigma = 1, SplitDistanceA(xe, xq); B: sigma = 1, Euclidean(xe, x) stored as B^T;
+      // C: sigma, SplitDistanceC(x, xq)  (src/split_kernel.jl:151-159)
+      GPR_TRY(launch_pair(ctx, 1, d, xes + (size_t)p * d * E, E, xqs + (size_t)p * d * nq, nq, 1.0,
+                          A + p * szA, 1, E));
+      GPR_TRY(launch_pair(ctx, 0, d, xes + (size_t)p * d * E, E, xs + (size_t)p * d * ns, ns, 1.0,
+                          BT + p * szB, ns, 1));
+      GPR_TRY(launch_pair(ctx, 2, d, xs + (size_t)p * d * ns, ns, xqs + (size_t)p * d * nq, nq, s2,
+                          C + p * szC, 1, ns));
+    }
+  }
+  // ---- mean: mu[e, q] = sum_p A_p[e,q] * (B_p diag(wt) C_p)[e,q]  (src/split_predict.jl:10-19)
+  for (int p = 0; p < nse; ++p) {
+    GemmArgs g{};
+    g.P = BT + p * szB; g.ldp = ns;
+    g.Q = C + p * szC; g.ldq = ns;
+    g.qscale = dwt;
+    g.E = A + p * szA; g.lde = E;
+    g.C = dmu + e_lo; g.ldc = ne;
+    g.M = E; g.N = nq; g.K = ns;
+    g.alpha = 1.0; g.beta = (p == 0) ? 0.0 : 1.0;
+    GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+  }
+  // ---- variance: prior everywhere in range, then rows e in [var_lo, var_hi) updated
+  const double prior = diag_prior(kinds, nk, hp, d);
+  GPR_TRY(launch_fill(ctx, dvar + (size_t)e_lo * nq, (size_t)E * nq, prior));
+  const int v0 = std::max(var_lo, e_lo), v1 = std::min(var_hi, e_hi);
+  if (v1 > v0) {
+    const size_t per_row = (size_t)ns * nq;
+    int Eb = (int)std::max<size_t>(1, ((size_t)1 << 28) / per_row);  // <= 2 GiB of RHS per batch
+    Eb = std::min(Eb, v1 - v0);
+    GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per_row * Eb));
+    for (int e = v0; e < v1; e += Eb) {
+      const int nr = std::min(Eb, v1 - e);
+      {
+        TimerScope ts(ctx, TC_OTHER, 0.0);
+        const size_t total = per_row * nr;
+        int blocks = (int)std::min<size_t>((total + 255) / 256, 65536);
+        split_kxq_kernel<<<blocks, 256, 0, ctx->stream>>>(nse, A, BT, C, ns, nq, E, e - e_lo, nr,
+                                                          ctx->dbig);
+        LAUNCH_CHECK(ctx);
+      }
+      GPR_TRY(trsm_ut_core(ctx, dU, ns, ldu, ctx->dbig, nr * nq, ns, dvar + (size_t)e * nq, 0));
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,42 @@
+"""gpr_amd -- MI355X-native drop-in for the dense exact-GP hot path of
+GaussianProcessRegression.jl.
+
+Names and argument meaning follow the reference's exported API
+(src/GaussianProcessRegression.jl:16-84); Julia's mutating ``f!`` functions are spelled
+``f_`` here.  Every numeric operation runs in libgpr_hip.so (hand-written gfx950 HIP); there
+is no CPU fallback.
+"""
+from ._lib import GPR_PREDICT_DIAG, GPR_PREDICT_FULL, GPR_PREDICT_MEAN, GprError, PosDefException
+from .core import (
+    Cmap,
+    ComposedKernel,
+    Context,
+    GPRModel,
+    GPRPredictCache,
+    GPRSplitPredictCache,
+    LogScale,
+    MarginalLikelihood,
+    MllGradCache,
+    MllLossCache,
+    NoLogScale,
+    SquaredExp,
+    UniformScaling,
+    WhiteNoise,
+    default_context,
+    dim_hp,
+    get_sample,
+    grad,
+    grad_,
+    islog,
+    kernel,
+    log_loss_grad_,
+    loss,
+    loss_grad_,
+    predict,
+    predict_,
+    predict_mean,
+    split_factors,
+    update_cache_,
+)
+
+__all__ = [n for n in dir() if not n.startswith("_")]

@@ -1,0 +1,180 @@
+/*
+ * gpr_hip.h -- C ABI of libgpr_hip.so, the MI355X (gfx950) exact-GP engine.
+ *
+ * Drop-in boundary for the dense hot path of GaussianProcessRegression.jl
+ * (reference snapshot 2025-03-21).  The reference has no FFI of its own: its extension
+ * seams are Julia multiple dispatch on the output-array type (kernel!(::AbstractGPUArray)
+ * src/covar_gpu.jl:1) and on the cache type (update_cache!/loss/grad!/predict!,
+ * src/cost.jl:40-126, src/predict.jl:29-101, src/split_predict.jl:5-53).  Each entry point
+ * below names the reference function it replaces; INTEGRATION.md shows the Julia
+ * `ccall` methods a maintainer adds on those seams.
+ *
+ * Conventions (all of them Julia's, so a Julia caller passes its arrays unchanged):
+ *   - fp64 everywhere; matrices are COLUMN-MAJOR with an explicit leading dimension.
+ *   - x is d x n column-major (each sample's d features contiguous), like md.x.
+ *   - A kernel is described by `kinds[nk]` (GPR_SE / GPR_WN, in `+` order) and the flat
+ *     hyper-parameter vector `hp` (HOST pointer) of length sum(dim_hp) -- SE: d+1
+ *     ([sigma, l_1..l_d]), WN: 1 ([sigma_n]) -- exactly split(hp, dims)
+ *     (src/compose_covar.jl:21-28).
+ *   - Pointers named d* are DEVICE pointers (from gpr_malloc, hipMalloc, or a torch
+ *     tensor); all other pointers are host pointers.  No pointer is retained after a call
+ *     returns.
+ *   - Every op is enqueued on the context's stream.  Ops that return host scalars/vectors
+ *     (info, mll, grad) synchronise the stream before returning; the others are async.
+ *   - A context is not thread-safe: one context (one stream) per host thread.
+ *
+ * Return codes: 0 ok; >0 LAPACK-style info (gpr_potrf_upper: order of the leading minor
+ * that is not positive definite, like dpotrf / Julia's PosDefException(info));
+ * <0 errors (GPR_E_*), with a message from gpr_last_error(ctx).
+ */
+#ifndef GPR_HIP_H
+#define GPR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPR_SE 1 /* SquaredExp  src/covariance.jl:15 */
+#define GPR_WN 2 /* WhiteNoise  src/covariance.jl:17 */
+
+#define GPR_OK 0
+#define GPR_E_ARG (-1)      /* bad argument (message names it)                      */
+#define GPR_E_HIP (-2)      /* HIP runtime error                                    */
+#define GPR_E_NOMEM (-3)    /* device allocation failed                             */
+#define GPR_E_UNSUP (-4)    /* unsupported configuration (e.g. d > GPR_MAX_DIM)      */
+
+#define GPR_MAX_DIM 64      /* max input dimension d                               */
+#define GPR_MAX_PARTS 8     /* max kernel parts in a composed kernel                */
+
+/* predict modes (src/predict.jl:14-25) */
+#define GPR_PREDICT_MEAN 0  /* predict_mean  src/predict.jl:6-12                     */
+#define GPR_PREDICT_DIAG 1  /* predict(...; diagonal_var=true)                       */
+#define GPR_PREDICT_FULL 2  /* predict(...; diagonal_var=false)                      */
+
+typedef struct gpr_ctx* gpr_ctx_t;
+
+/* ---- context & memory ------------------------------------------------------------- */
+/* stream: a hipStream_t to run on (NULL = the context creates its own non-blocking one). */
+int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out);
+int gpr_ctx_destroy(gpr_ctx_t ctx);
+const char* gpr_last_error(gpr_ctx_t ctx);
+const char* gpr_version(void);
+int gpr_sync(gpr_ctx_t ctx);
+void* gpr_ctx_stream(gpr_ctx_t ctx);
+int gpr_malloc(gpr_ctx_t ctx, size_t bytes, void** dptr);
+int gpr_free(gpr_ctx_t ctx, void* dptr);
+int gpr_upload(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes);   /* sync H2D */
+int gpr_download(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes); /* sync D2H */
+/* Panel width of the blocked factorisations (default 128).  Must be a multiple of 64. */
+int gpr_set_block(gpr_ctx_t ctx, int nb);
+/* Per-kernel-class timing with HIP events on the context stream (bench instrumentation).
+ * class: 0 K-assembly, 1 POTRF trailing update (SYRK), 2 POTRF panel (diag+TRSM),
+ *        3 TRSM trailing GEMM, 4 other.  Returns accumulated ms, launch count, flops. */
+int gpr_timing_enable(gpr_ctx_t ctx, int on);
+int gpr_timing_get(gpr_ctx_t ctx, int cls, double* ms, long long* launches, double* flops);
+int gpr_timing_reset(gpr_ctx_t ctx);
+
+/* ---- a2/a3: kernel matrices --------------------------------------------------------- */
+/* K[n x m] (ldk) = kernel(cov, hp, x, xp).  same != 0 means `x === xp`
+ * (then dXp is ignored, m must equal n): +eps on the diagonal once per SE part and
+ * +sigma_n^2 of the first WhiteNoise part.  same == 0: cross kernel, no eps, no noise.
+ * Replaces kernel!(kern, ::SquaredExp, hp, x, xp) src/covariance.jl:49-58,85-95,
+ * kernel!(kern::AbstractGPUArray, ...) src/covar_gpu.jl:1-18 and
+ * kernel!(kern, ::ComposedKernel, hp, x[, xp]) src/compose_covar.jl:47-77. */
+int gpr_kernel(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+               const double* dX, int n, const double* dXp, int m, int same, double eps,
+               double* dK, int ldk);
+
+/* a4: dK/dtheta_i (1-based i) materialised, n x n.  WN part: writes 2*sigma_n*I.
+ * Replaces grad!(::SquaredExp, DK, i, hp, x, K) src/deriv_covar.jl:20-32 and the
+ * composed index mapping src/compose_covar.jl:109-123. */
+int gpr_kernel_grad(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                    const double* dX, int n, int i, double eps, double* dDK, int ld);
+
+/* ---- a5-a7: factor / solve --------------------------------------------------------- */
+/* In-place upper Cholesky of the SPD matrix in dA (n x n, lda): upper triangle <- U with
+ * K = U^T U, strict lower triangle untouched.  *info = 0 or the order of the failing
+ * minor.  Replaces cholesky!(Hermitian(K)) = dpotrf('U') (src/cost.jl:77,87,104,
+ * src/predict.jl:31).  The context keeps the inverses of the diagonal blocks for the
+ * following gpr_potrs/gpr_trsm/gpr_potri calls on the same factor. */
+int gpr_potrf_upper(gpr_ctx_t ctx, double* dA, int n, int lda, int* info);
+
+/* B <- K^{-1} B for K = U^T U (dU from gpr_potrf_upper), B n x nrhs (ldb).
+ * Replaces ldiv!(alpha, kchol, y) = dpotrs (src/cost.jl:79,89,106, src/predict.jl:32). */
+int gpr_potrs_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
+                    int ldb);
+
+/* B <- U^{-T} B (left, upper, transposed triangular solve).  With B = K(x, xp)^T this is
+ * rdiv!(Kxp, kchol.U) (src/predict.jl:84,90,98) in the transposed layout. */
+int gpr_trsm_upper_trans(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dB,
+                         int nrhs, int ldb);
+
+/* Full symmetric K^{-1} (n x n, ldk) from the factor.  Replaces
+ * K^-1 = I ; ldiv!(kchol, K^-1) (src/cost.jl:90-92,107-109). */
+int gpr_potri_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dKinv, int ldk);
+
+/* ---- a8/a9: marginal likelihood ------------------------------------------------------ */
+/* *out = 0.5 (y.alpha + 2 sum log U_ii + n log 2pi)  (src/loss_grad.jl:39-41). */
+int gpr_mll(gpr_ctx_t ctx, const double* dU, int n, int ldu, const double* dy,
+            const double* dalpha, double* out);
+
+/* grad[D] (host) of the negative log-marginal-likelihood w.r.t. hp, fused over all D
+ * hyper-parameters in one pass over the upper triangle of K^{-1} (never materialising
+ * dK): g_i = -0.5 sum_ab (alpha_a alpha_b - Kinv_ab) dK_i,ab.  Replaces the grad! loop of
+ * src/cost.jl:119-126 with src/loss_grad.jl:43-52 and src/deriv_covar.jl:20-32.
+ * log_scale != 0 applies G .*= hp (src/cost.jl:60-70). */
+int gpr_mll_grad(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                 const double* dX, int n, const double* dKinv, int ldk,
+                 const double* dalpha, double eps, int log_scale, double* grad);
+
+/* One-call fit = update_cache!(MllLossCache / GPRPredictCache) (src/cost.jl:74-81,
+ * src/predict.jl:29-34): dK (n x n, ldk) <- kernel, then in-place POTRF, then
+ * dalpha <- K^{-1} dy (nrhs columns, ldy).  Returns info > 0 if not PD. */
+int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+            const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
+            double* dK, int ldk, double* dalpha, int* info);
+
+/* ---- a10/a11: posterior ------------------------------------------------------------ */
+/* Posterior at m test points from a fitted factor (dU, dwt = K^{-1} y with nrhs cols).
+ * mode GPR_PREDICT_MEAN: dmu (m x nrhs, ldmu=m).  GPR_PREDICT_DIAG: + dvar[m] =
+ * prior - ||U^{-T} k_j||^2 (prior sigma^2 or sum of all parts' hp[1]^2, no eps:
+ * src/predict.jl:51-71,89-95).  GPR_PREDICT_FULL: + dvar (m x m, ldv) = K(xp,xp) -
+ * V^T V (src/predict.jl:42-49,83-87).  dwork: optional device scratch of n*m doubles
+ * (NULL: the context allocates it).  Replaces predict!/predict_mean! src/predict.jl. */
+int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                const double* dX, int n, const double* dU, int ldu, const double* dwt,
+                int nrhs, const double* dXp, int m, int mode, double eps, double* dmu,
+                double* dvar, int ldv, double* dwork);
+
+/* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
+/* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).
+ * dmu: ne x nq column-major (index e + q*ne, src/split_predict.jl:10-19).
+ * dvar: ne*nq diagonal; entries (e*nq + q) for e in [var_lo, var_hi) (0-based,
+ * half-open; the reference default var_range=1:3 is [0,3)) get prior - ||U^{-T} k||^2,
+ * every other entry is set to the prior (src/split_predict.jl:39-53).
+ * e_lo/e_hi restrict the call to grid rows [e_lo, e_hi) (multi-GPU sharding: each rank
+ * passes its own row range; dmu/dvar still index the FULL grid layout, only the rows in
+ * range are written).  dwt is the 1-column K^{-1} y.
+ * Replaces kernel!(::SplitKernel,...) src/split_kernel.jl:137-159 and
+ * predict_split_mean_impl!/predict_covar_impl! src/split_predict.jl:5-53. */
+int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                      const double* dX, int ns, const double* dU, int ldu,
+                      const double* dwt, const double* dXe, int ne, const double* dXq,
+                      int nq, int e_lo, int e_hi, int var_lo, int var_hi, double eps,
+                      double* dmu, double* dvar);
+
+/* Split factors for inspection/tests (src/split_kernel.jl:151-159), SE part `part`
+ * (0-based among SE parts): dA ne x nq, dB ne x ns, dC ns x nq (column-major,
+ * leading dims = row counts). */
+int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                      const double* dX, int ns, const double* dXe, int ne,
+                      const double* dXq, int nq, int part, double* dA, double* dB,
+                      double* dC);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPR_HIP_H */

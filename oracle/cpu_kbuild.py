@@ -1,0 +1,45 @@
+"""ctypes wrapper of oracle/_build/libkbuild_cpu.so (threaded C K-assembly restatement).
+
+TEST INFRASTRUCTURE ONLY: used by tests/ and by bench.py's cpu_baseline leg."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import gpr_oracle as O
+
+_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libkbuild_cpu.so")
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(_LIB)
+        D = ctypes.POINTER(ctypes.c_double)
+        _lib.kbuild_cpu.argtypes = [ctypes.c_int, ctypes.c_int, D, ctypes.c_int, D, ctypes.c_int,
+                                    D, D, ctypes.c_int, ctypes.c_double, ctypes.c_double, D]
+        _lib.kbuild_cpu.restype = None
+    return _lib
+
+
+def kbuild_cpu(kinds, hp, x, xp=None, eps=O.EPS_DEFAULT) -> np.ndarray:
+    """Same result as oracle.gpr_oracle.kernel(kinds, hp, x, xp, eps), OpenMP-threaded."""
+    lib = _load()
+    d, n = x.shape
+    hps = O.split_hp(kinds, np.asarray(hp, dtype=np.float64), d)
+    se = [h for k, h in zip(kinds, hps) if k == O.SE]
+    wn = [h for k, h in zip(kinds, hps) if k == O.WN]
+    sig = np.array([h[0] for h in se], dtype=np.float64)
+    ls = np.ascontiguousarray(np.stack([h[1:] for h in se]), dtype=np.float64)
+    xc = np.ascontiguousarray(x.T)  # column-major d x n
+    m = n if xp is None else xp.shape[1]
+    K = np.empty((m, n), dtype=np.float64)  # row-major (m, n) == column-major n x m
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    xpc = None if xp is None else np.ascontiguousarray(xp.T)
+    lib.kbuild_cpu(d, n, P(xc), m, None if xp is None else P(xpc), len(se), P(sig), P(ls),
+                   1 if (wn and xp is None) else 0, float(wn[0][0] ** 2) if wn else 0.0, eps,
+                   P(K))
+    return K.T

@@ -1,0 +1,371 @@
+"""CPU oracle: NumPy/SciPy fp64 restatement of GaussianProcessRegression.jl's dense hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker / the timed CPU
+baseline -- never as the thing measured or shipped.  The product path
+(``gaussianprocessregression.jl_amd/gpr_amd``) never imports it and fails loudly when the
+HIP library is missing.
+
+Pinning: the reference is Julia (not installed here; its LazyTensors dependency is an
+unregistered GitHub package that cannot be fetched offline), so it cannot be run to
+produce golden vectors, and its test-suite holds no golden data.  This restatement is
+pinned against every known-answer / identity test the reference's own suite contains
+(see ``tests/test_oracle.py``): the closed-form diagonal-K MLL (test/test_loss.jl:1-11),
+the grad identity with dK=K (test/test_loss.jl:32), cache contents vs fresh cholesky/inv
+(test/test_loss.jl:46-48), FD gradients (test/test_loss.jl:13-20,50-55;
+test/test_covariance.jl:3-9,84-87), kernel composition identities
+(test/test_covariance.jl:34-105), interpolation at the training points
+(test/test_models.jl:17-32), diag-vs-full variance (test/test_models.jl:34-48), the split
+distance / split kernel / split predict identities (test/test_split_kernel.jl), plus a
+50-digit mpmath recomputation at small N bounding the oracle's own rounding error.
+
+Conventions follow the reference exactly (Julia, column-major):
+  * ``x`` is d x N (each sample's d features contiguous), ``hp`` a flat vector whose
+    layout is the concatenation over kernel parts in ``+`` order
+    (src/compose_covar.jl:21-28).
+  * SE part hp = [sigma, l_1..l_d]; K = sigma^2 exp(-sum_k (l_k x_k - l_k x'_k)^2)
+    (src/covariance.jl:8-12,85-95) -- l multiplies, no 1/2.
+  * eps = 1e-8 is added to the diagonal, once per SE part, iff the two inputs are the
+    same object (src/covariance.jl:49-58, src/compose_covar.jl:47-61).
+All arrays here are numpy arrays in the same (row, col) index convention as Julia; the
+memory order is irrelevant to the oracle.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import scipy.linalg as sla
+
+SE = "SE"
+WN = "WN"
+EPS_DEFAULT = 1e-8
+LOG2PI = math.log(2.0 * math.pi)
+
+
+# ---------------------------------------------------------------------------------------
+# Kernel specs (src/covariance.jl:15-27,60; src/compose_covar.jl:1-28)
+# ---------------------------------------------------------------------------------------
+def dim_hp(kind: str, d: int) -> int:
+    """src/covariance.jl:27 (SE: d+1), :60 (WN: 1)."""
+    if kind == SE:
+        return d + 1
+    if kind == WN:
+        return 1
+    raise ValueError(kind)
+
+
+def split_hp(kinds: Sequence[str], hp: np.ndarray, d: int) -> List[np.ndarray]:
+    """Base.split(hp, dims) src/compose_covar.jl:21-24 with dims from :26-28."""
+    dims = [dim_hp(k, d) for k in kinds]
+    if sum(dims) != len(hp):
+        raise ValueError("Parameter size mismatch.")  # src/models.jl:27
+    out, c = [], 0
+    for n in dims:
+        out.append(np.asarray(hp[c:c + n], dtype=np.float64))
+        c += n
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Distances and SE kernel (src/covariance.jl:72-95)
+# ---------------------------------------------------------------------------------------
+def distance_euclid(xs: np.ndarray, xps: np.ndarray) -> np.ndarray:
+    """distance!(Euclidean) src/covariance.jl:72-77: D[a,b] = sum_k (x[k,a]-x'[k,b])^2."""
+    D = np.zeros((xs.shape[1], xps.shape[1]))
+    for k in range(xs.shape[0]):  # sum over dim 1, feature by feature
+        D += (xs[k][:, None] - xps[k][None, :]) ** 2
+    return D
+
+
+def se_kernel(hp: np.ndarray, x: np.ndarray, xp: np.ndarray, same: bool,
+              eps: float = EPS_DEFAULT, dist: str = "euclid") -> np.ndarray:
+    """kernel!(kern, ::SquaredExp, hp, x, xp) src/covariance.jl:49-58 -> kernel_impl! :85-95.
+
+    Scale-then-difference: xs = x .* l, D = distance(xs, xps), K = sigma^2 * exp(-1.0*D);
+    +eps on the diagonal iff x === xp.  ``dist`` selects the split metrics of
+    src/split_kernel.jl:108-123.
+    """
+    sigma, ls = hp[0], hp[1:]
+    xs = x * ls[:, None]
+    xps = xp * ls[:, None]
+    if dist == "euclid":
+        D = distance_euclid(xs, xps)
+    elif dist == "splitA":
+        D = split_distance_a(xs, xps)
+    elif dist == "splitC":
+        D = split_distance_c(xs, xps)
+    else:
+        raise ValueError(dist)
+    K = (sigma ** 2) * np.exp(-1.0 * D)
+    if same:
+        K[np.diag_indices(K.shape[0])] += eps
+    return K
+
+
+def kernel(kinds: Sequence[str], hp: np.ndarray, x: np.ndarray, xp: np.ndarray | None = None,
+           eps: float = EPS_DEFAULT) -> np.ndarray:
+    """Composed / single kernel matrix.
+
+    kernel!(kern, K::ComposedKernel, hp, x)       src/compose_covar.jl:73-77 (same, + noise)
+    kernel!(kern, K::ComposedKernel, hp, x, xp)   src/compose_covar.jl:47-61 (cross, no noise)
+    Summation order: first SE part, then `kern .+= kernel(part_t)` for t = 2.. (each SE
+    part carries its own +eps when same), then add_noise! (:63-71) adds sigma_n^2.
+    """
+    d = x.shape[0]
+    same = xp is None
+    xq = x if same else xp
+    hps = split_hp(kinds, hp, d)
+    se_idx = [i for i, k in enumerate(kinds) if k == SE]   # rm_noise :30-33
+    if not se_idx:
+        raise ValueError("kernel needs at least one SquaredExp part")
+    K = se_kernel(hps[se_idx[0]], x, xq, same, eps)
+    for i in se_idx[1:]:
+        K = K + se_kernel(hps[i], x, xq, same, eps)
+    if same and WN in kinds:
+        nidx = kinds.index(WN)  # findfirst: only the first WhiteNoise counts (:64-68)
+        K[np.diag_indices(K.shape[0])] += hps[nidx][0] ** 2
+    return K
+
+
+def kernel_grad(kinds: Sequence[str], i: int, hp: np.ndarray, x: np.ndarray,
+                eps: float = EPS_DEFAULT):
+    """grad(cov, i, hp, x): src/deriv_covar.jl:2-32 + composed find_idx src/compose_covar.jl:109-123.
+
+    ``i`` is 1-based like Julia.  SE: i==1 -> (2/|sigma|) K (K incl. eps on diag);
+    i>1 -> -2 l_{i-1} K (x_{i-1,a}-x_{i-1,b})^2 with RAW x.  WN: 2 sigma_n I, returned as
+    the tuple ("I", lambda).
+    """
+    d = x.shape[0]
+    hps = split_hp(kinds, hp, d)
+    dims = np.cumsum([dim_hp(k, d) for k in kinds])
+    kidx = int(np.searchsorted(dims, i))  # first cdims >= i
+    hpidx = i if kidx == 0 else i - dims[kidx - 1]
+    part = hps[kidx]
+    if kinds[kidx] == WN:
+        return ("I", 2.0 * part[0])
+    Kp = se_kernel(part, x, x, True, eps)
+    if hpidx == 1:
+        return (2.0 / abs(part[0])) * Kp
+    k = hpidx - 2
+    diff2 = (x[k][:, None] - x[k][None, :]) ** 2
+    return -2.0 * part[hpidx - 1] * Kp * diff2
+
+
+# ---------------------------------------------------------------------------------------
+# Cholesky-based MLL (src/cost.jl:74-126, src/loss_grad.jl:32-52)
+# ---------------------------------------------------------------------------------------
+def chol_upper(K: np.ndarray) -> np.ndarray:
+    """cholesky!(Hermitian(K)) = LAPACK dpotrf('U'): K = U^T U (src/cost.jl:77)."""
+    return sla.cholesky(K, lower=False, check_finite=False)
+
+
+def potrf_inplace_upper(K: np.ndarray) -> np.ndarray:
+    """What the in-place dpotrf('U') leaves in the buffer: U in the upper triangle, the
+    original K in the strict lower triangle (test/test_loss.jl:46)."""
+    U = chol_upper(K)
+    out = np.tril(K, -1) + np.triu(U)
+    return out
+
+
+def cho_solve_upper(U: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """ldiv!(alpha, kchol, y) = dpotrs (src/cost.jl:79)."""
+    z = sla.solve_triangular(U, y, trans="T", lower=False, check_finite=False)
+    return sla.solve_triangular(U, z, trans="N", lower=False, check_finite=False)
+
+
+def kinv_from_upper(U: np.ndarray) -> np.ndarray:
+    """K^{-1} = ldiv!(kchol, I) (src/cost.jl:90-92): dpotrs with N right-hand sides."""
+    return cho_solve_upper(U, np.eye(U.shape[0]))
+
+
+def get_sample(y: np.ndarray, train_axis: int = 1) -> np.ndarray:
+    """src/models.jl:39-45 (train_axis is 1-based)."""
+    return y if y.ndim == 1 else y[:, train_axis - 1]
+
+
+def mll_value(U: np.ndarray, y: np.ndarray, alpha: np.ndarray) -> float:
+    """loss(MLL, kchol, y, K^-1 y) src/loss_grad.jl:39-41: 0.5(y.alpha + logdet + N log 2pi).
+
+    logdet(Cholesky) = 2 sum log U_ii.
+    """
+    n = U.shape[0]
+    return 0.5 * (float(np.dot(y, alpha)) + 2.0 * float(np.sum(np.log(np.diag(U)))) + n * LOG2PI)
+
+
+def mll(kinds, hp, x, y, eps=EPS_DEFAULT, train_axis=1):
+    """loss(MLL, hp, md) src/cost.jl:19-22,40-43,74-81,113-117."""
+    K = kernel(kinds, hp, x, None, eps)
+    U = chol_upper(K)
+    ys = get_sample(y, train_axis)
+    alpha = cho_solve_upper(U, ys)
+    return mll_value(U, ys, alpha)
+
+
+def mll_grad_term(dK, alpha: np.ndarray, Kinv: np.ndarray) -> float:
+    """grad(MLL, kchol, dK, alpha, K^-1, tt) src/loss_grad.jl:43-52."""
+    if isinstance(dK, tuple):  # UniformScaling
+        return -0.5 * dK[1] * float(np.sum(alpha ** 2 - np.diag(Kinv)))
+    tt = dK @ alpha
+    return -0.5 * (float(np.dot(tt, alpha)) - float(np.sum(Kinv * dK)))
+
+
+def mll_grad(kinds, hp, x, y, eps=EPS_DEFAULT, train_axis=1, log_scale=False):
+    """grad!(dL, MLL, hp, md, tc) src/cost.jl:45-48,83-111,119-126; log_loss_grad! :60-70.
+
+    Returns the D-vector; with log_scale=True the chain rule G .*= hp is applied.
+    """
+    hp = np.asarray(hp, dtype=np.float64)
+    K = kernel(kinds, hp, x, None, eps)
+    U = chol_upper(K)
+    ys = get_sample(y, train_axis)
+    alpha = cho_solve_upper(U, ys)
+    Kinv = kinv_from_upper(U)
+    g = np.empty(len(hp))
+    for i in range(1, len(hp) + 1):
+        g[i - 1] = mll_grad_term(kernel_grad(kinds, i, hp, x, eps), alpha, Kinv)
+    if log_scale:
+        g = g * hp
+    return g
+
+
+def islog(kinds) -> bool:
+    """islog(MLL, md) src/cost.jl:4-8: LogScale iff a SquaredExp part is present."""
+    return SE in kinds
+
+
+# ---------------------------------------------------------------------------------------
+# Posterior (src/predict.jl)
+# ---------------------------------------------------------------------------------------
+def diag_prior(kinds, hp, d) -> float:
+    """Diagonal-variance prior: SE alone sigma^2 (src/predict.jl:67); composed: sum over
+    ALL parts of hp_part[1]^2 incl. the noise (src/predict.jl:56-58).  No eps."""
+    hps = split_hp(kinds, hp, d)
+    if len(kinds) == 1:
+        return float(hps[0][0] ** 2)
+    return float(sum(h[0] ** 2 for h in hps))
+
+
+def predict(kinds, hp, x, y, xp, diagonal_var=False, eps=EPS_DEFAULT):
+    """predict(md, xp; diagonal_var) src/predict.jl:14-25 with update_cache! :29-34,
+    predict! :42-71, predict_mean_impl! :73-76, predict_covar_impl! :83-95.
+
+    Returns (mu, Sigma) with Sigma an np x np matrix (full) or the np diagonal vector.
+    """
+    d = x.shape[0]
+    K = kernel(kinds, hp, x, None, eps)
+    U = chol_upper(K)
+    wt = cho_solve_upper(U, y)                    # ldiv!(pc.wt, kchol, md.y)
+    Kxp = kernel(kinds, hp, xp, x, eps)           # np x N cross kernel (no eps, no noise)
+    mu = Kxp @ wt
+    V = sla.solve_triangular(U, Kxp.T, trans="T", lower=False, check_finite=False).T  # rdiv!(Kxp,U)
+    if diagonal_var:
+        var = diag_prior(kinds, hp, d) - np.sum(V * V, axis=1)
+        return mu, var
+    S = kernel(kinds, hp, xp, None, eps)          # kernel!(Sigma, covar, hp, xp): eps (+noise)
+    S = S - V @ V.T
+    return mu, S
+
+
+# ---------------------------------------------------------------------------------------
+# Split kernel / split prediction (src/split_kernel.jl, src/split_predict.jl)
+# ---------------------------------------------------------------------------------------
+def cmap_points(xe: np.ndarray, xq: np.ndarray) -> np.ndarray:
+    """Cmap(+, xe, xq)[:, :] src/split_kernel.jl:1-17: column index e + (q-1)*ne (1-based),
+    i.e. e fastest (test/test_split_kernel.jl:20-21)."""
+    d, ne = xe.shape
+    nq = xq.shape[1]
+    return (xe[:, :, None] + xq[:, None, :]).reshape(d, ne * nq, order="F")
+
+
+def split_distance_a(xe: np.ndarray, xq: np.ndarray) -> np.ndarray:
+    """distance!(SplitDistanceA) src/split_kernel.jl:111-116: sum_k xq^2 + 2 xe xq."""
+    D = np.zeros((xe.shape[1], xq.shape[1]))
+    for k in range(xe.shape[0]):
+        D += xq[k][None, :] ** 2 + 2.0 * xe[k][:, None] * xq[k][None, :]
+    return D
+
+
+def split_distance_c(xs: np.ndarray, xq: np.ndarray) -> np.ndarray:
+    """distance!(SplitDistanceC) src/split_kernel.jl:118-123: sum_k -2 xs xq."""
+    D = np.zeros((xs.shape[1], xq.shape[1]))
+    for k in range(xs.shape[0]):
+        D += -2.0 * xs[k][:, None] * xq[k][None, :]
+    return D
+
+
+def split_factors(kinds, hp, x, xe, xq, eps=EPS_DEFAULT):
+    """kernel!(SplitKernel, ...) src/split_kernel.jl:137-159: per SE part k,
+    A[:,:,k] (ne x nq, sigma=1, SplitDistanceA), B[:,:,k] (ne x ns, sigma=1, Euclidean),
+    C[:,:,k] (ns x nq, sigma, SplitDistanceC).  None of them is a same-object call, so no
+    eps is added."""
+    d = x.shape[0]
+    hps = split_hp(kinds, hp, d)
+    parts = [hps[i] for i, k in enumerate(kinds) if k == SE]
+    A, B, C = [], [], []
+    for h in parts:
+        h1 = h.copy()
+        h1[0] = 1.0
+        A.append(se_kernel(h1, xe, xq, False, eps, dist="splitA"))
+        B.append(se_kernel(h1, xe, x, False, eps, dist="euclid"))
+        C.append(se_kernel(h, x, xq, False, eps, dist="splitC"))
+    return np.stack(A, 2), np.stack(B, 2), np.stack(C, 2)
+
+
+def split_predict(kinds, hp, x, y, xe, xq, var_range: Tuple[int, int] | None = (1, 3),
+                  eps=EPS_DEFAULT):
+    """predict(md, Cmap(+,xe,xq); diagonal_var=true) src/predict.jl:14-25,51-71 with
+    predict_split_mean_impl! src/split_predict.jl:10-19 and the split
+    predict_covar_impl! :39-53 (var_range default 1:3, src/caches/split_kernel.jl:10).
+
+    Returns mu as an ne x nq matrix (column-major linear index e + (q-1) ne) and the
+    variance diagonal of length ne*nq whose entry (e-1)*nq + q is updated only for
+    e in var_range (1-based inclusive); every other entry keeps the prior.
+    """
+    d = x.shape[0]
+    ne, nq = xe.shape[1], xq.shape[1]
+    K = kernel(kinds, hp, x, None, eps)
+    U = chol_upper(K)
+    wt = cho_solve_upper(U, y)
+    A, B, C = split_factors(kinds, hp, x, xe, xq, eps)
+    mu = np.zeros((ne, nq))
+    for k in range(A.shape[2]):
+        Cw = wt[:, None] * C[:, :, k]
+        BCw = B[:, :, k] @ Cw
+        mu += BCw * A[:, :, k]
+    var = np.full(ne * nq, diag_prior(kinds, hp, d))
+    if var_range is not None:
+        lo, hi = var_range
+        lo, hi = max(lo, 1), min(hi, ne)
+        for e in range(lo, hi + 1):
+            Kxq = np.zeros((nq, x.shape[1]))
+            for k in range(A.shape[2]):
+                Kxq += A[e - 1, :, None, k] * B[e - 1, None, :, k] * C[:, :, k].T
+            V = sla.solve_triangular(U, Kxq.T, trans="T", lower=False, check_finite=False).T
+            var[(e - 1) * nq:e * nq] -= np.sum(V * V, axis=1)
+    return mu, var
+
+
+# ---------------------------------------------------------------------------------------
+# Synthetic data
+# ---------------------------------------------------------------------------------------
+def synthetic(d: int, n: int, npred: int = 0, seed_train: int = 0, seed_test: int = 1):
+    """x = U[0,1)^(d x n), y = sin(sum_k x_k)^2 (test/test_models.jl:8)."""
+    x = np.random.default_rng(seed_train).random((d, n))
+    y = np.sin(np.sum(x, axis=0)) ** 2
+    xp = np.random.default_rng(seed_test).random((d, npred)) if npred else None
+    return x, y, xp
+
+
+def default_hp(kinds, d, length=None, sigma=1.0, noise=0.1):
+    """sigma=1, l_k = 3 sqrt(8/d), sigma_n = 0.1."""
+    l = 3.0 * math.sqrt(8.0 / d) if length is None else length
+    hp = []
+    for k in kinds:
+        if k == SE:
+            hp += [sigma] + [l] * d
+        else:
+            hp += [noise]
+    return np.array(hp, dtype=np.float64)

@@ -1,0 +1,456 @@
+"""GPU parity: libgpr_hip.so (through the C ABI, via gpr_amd) vs the CPU oracle.
+
+Each test restates one of the reference's own tests (file:line cited) and/or compares the
+HIP result with the oracle on identical seeded inputs.  Tolerances (fp64):
+  kernel matrices   rtol 1e-13 (pure elementwise arithmetic + exp)
+  factor / inverse  normwise 1e-11 (well-conditioned inputs)
+  posterior, MLL    rtol 1e-8 (BASELINE north_star) -- observed errors are far smaller
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+from oracle import gpr_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+G = pytest.importorskip("gpr_amd")
+
+SE, WN = O.SE, O.WN
+KSETS = {
+    "SE": [SE],
+    "SE+WN": [SE, WN],
+    "SE+SE": [SE, SE],
+    "SE+SE+WN": [SE, SE, WN],
+    "WN+SE": [WN, SE],
+    "SE+WN+SE": [SE, WN, SE],
+}
+
+
+def cov_of(kinds):
+    parts = [G.SquaredExp() if k == SE else G.WhiteNoise() for k in kinds]
+    c = parts[0]
+    for p in parts[1:]:
+        c = c + p
+    return c
+
+
+def rand_hp(kinds, d, rng, lo=0.3, hi=2.0):
+    return rng.uniform(lo, hi, sum(O.dim_hp(k, d) for k in kinds))
+
+
+def relnorm(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+# ---------------------------------------------------------------------------------------
+# a2/a3 kernel matrices  (test/test_covariance.jl:11-82)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", list(KSETS))
+@pytest.mark.parametrize("n,d", [(1, 1), (63, 2), (64, 3), (65, 5), (200, 7), (300, 8), (130, 16),
+                                 (97, 20)])
+def test_kernel_matrix(name, n, d):
+    kinds = KSETS[name]
+    rng = np.random.default_rng(n * 31 + d)
+    x = rng.random((d, n))
+    xp = rng.random((d, 2 * n))
+    hp = rand_hp(kinds, d, rng)
+    cov = cov_of(kinds)
+    K = G.kernel(cov, hp, x)
+    Ko = O.kernel(kinds, hp, x)
+    np.testing.assert_allclose(K, Ko, rtol=1e-13, atol=1e-15)
+    assert np.array_equal(K, K.T), "symmetric K must be bitwise symmetric (mirror of upper)"
+    Kx = G.kernel(cov, hp, x, xp)
+    np.testing.assert_allclose(Kx, O.kernel(kinds, hp, x, xp), rtol=1e-13, atol=1e-15)
+    assert Kx.shape == (n, 2 * n)
+
+
+def test_kernel_structure_isposdef():
+    """test/test_covariance.jl:27-32: issymmetric, isposdef, shapes."""
+    rng = np.random.default_rng(5)
+    for n in (100, 200, 300):
+        for dim in range(1, 8):
+            x = rng.random((dim, n))
+            hp = rng.random(dim + 1)
+            K = G.kernel(G.SquaredExp(), hp, x)
+            assert np.array_equal(K, K.T)
+            np.linalg.cholesky(K + 0.0)  # raises if not PD (eps jitter keeps it PD)
+
+
+def test_compose_identities():
+    """test/test_covariance.jl:34-81 restated against the HIP kernels."""
+    rng = np.random.default_rng(11)
+    dim, n = 3, 120
+    x, xp = rng.random((dim, n)), rng.random((dim, 2 * n))
+    SEk, WNk = G.SquaredExp(), G.WhiteNoise()
+    hps = rng.random(dim + 2)
+    np.testing.assert_allclose(G.kernel(SEk + WNk, hps, x),
+                               G.kernel(SEk, hps[:-1], x) + hps[-1] ** 2 * np.eye(n), rtol=1e-14)
+    np.testing.assert_allclose(G.kernel(SEk + WNk, hps, x, xp), G.kernel(SEk, hps[:-1], x, xp),
+                               rtol=1e-14)
+    hps = rng.random(2 * dim + 2)
+    np.testing.assert_allclose(G.kernel(SEk + SEk, hps, x),
+                               G.kernel(SEk, hps[:dim + 1], x) + G.kernel(SEk, hps[dim + 1:], x),
+                               rtol=1e-14)
+    hps = rng.random(2 * dim + 3)
+    np.testing.assert_allclose(
+        G.kernel(SEk + WNk + SEk, hps, x),
+        G.kernel(SEk, hps[:dim + 1], x) + G.kernel(SEk, hps[dim + 2:], x) + hps[dim + 1] ** 2 * np.eye(n),
+        rtol=1e-14)
+
+
+# ---------------------------------------------------------------------------------------
+# a4 dK/dtheta  (test/test_covariance.jl:3-9,84-105)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["SE", "SE+WN+SE"])
+def test_kernel_grad(name):
+    kinds = KSETS[name]
+    rng = np.random.default_rng(3)
+    dim, n = 2, 100
+    x = rng.random((dim, n))
+    hp = rand_hp(kinds, dim, rng)
+    cov = cov_of(kinds)
+    for i in range(1, len(hp) + 1):
+        g = G.grad(cov, i, hp, x)
+        go = O.kernel_grad(kinds, i, hp, x)
+        if isinstance(go, tuple):
+            assert isinstance(g, G.UniformScaling) and g.lam == pytest.approx(go[1])
+            continue
+        np.testing.assert_allclose(g, go, rtol=1e-12, atol=1e-14)
+        # forward FD, eps 1e-7, atol 1e-3 (test/test_covariance.jl:3-9,85)
+        hpe = hp.copy()
+        hpe[i - 1] += 1e-7
+        fd = (G.kernel(cov, hpe, x) - G.kernel(cov, hp, x)) / 1e-7
+        np.testing.assert_allclose(g, fd, atol=1e-3)
+
+
+# ---------------------------------------------------------------------------------------
+# a5 POTRF (dpotrf 'U', in place, lower untouched)
+# ---------------------------------------------------------------------------------------
+def _spd(n, d=4, seed=0, noise=0.3):
+    rng = np.random.default_rng(seed)
+    x = rng.random((d, n))
+    return O.kernel([SE, WN], np.r_[1.0, [1.5] * d, noise], x)
+
+
+def _dev_potrf(ctx, A, nb=None):
+    dA = ctx.colmajor(A)
+    n = A.shape[0]
+    info = ctypes.c_int(-7)
+    rc = G._lib.lib.gpr_potrf_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n, ctypes.byref(info))
+    assert rc >= 0, G._lib.lib.gpr_last_error(ctx.h)
+    return dA, info.value
+
+
+@pytest.mark.parametrize("n", [1, 50, 64, 127, 128, 129, 300, 700])
+@pytest.mark.parametrize("nb", [128, 64])
+def test_potrf_upper(n, nb):
+    ctx = G.Context(0, nb=nb)
+    A = _spd(n, seed=n)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    R = ctx.host(dA)
+    U = sla.cholesky(A, lower=False)
+    assert relnorm(np.triu(R), U) < 1e-12
+    # strict lower triangle untouched, bit for bit (test/test_loss.jl:46)
+    assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
+
+
+@pytest.mark.parametrize("j", [0, 5, 127, 128, 200])
+def test_potrf_not_posdef_info(j):
+    """Non-PD input: info = order of the failing leading minor (dpotrf / PosDefException)."""
+    ctx = G.Context(0)
+    A = _spd(260, seed=1)
+    A[j, j] = -1.0
+    _, info = _dev_potrf(ctx, A)
+    _, info_ref = sla.lapack.dpotrf(A, lower=0)
+    assert info == info_ref == j + 1
+
+
+def test_posdef_exception_from_model():
+    rng = np.random.default_rng(2)
+    x = rng.random((2, 50))
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), np.r_[1.0, 1.0, 1.0, 0.1], x, x[0])
+    md.params[0] = float("nan")
+    with pytest.raises(G.PosDefException):
+        G.loss(G.MarginalLikelihood(), md.params, md)
+
+
+# ---------------------------------------------------------------------------------------
+# a6/a7 solves, K^{-1}
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,nrhs", [(300, 1), (257, 3), (129, 20)])
+def test_potrs(n, nrhs):
+    ctx = G.Context(0)
+    A = _spd(n, seed=7)
+    dA, info = _dev_potrf(ctx, A)
+    B = np.random.default_rng(1).random((n, nrhs))
+    dB = ctx.colmajor(B)
+    rc = G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                   ctypes.c_void_p(dB.data_ptr()), nrhs, n)
+    assert rc == 0
+    X = ctx.host(dB)
+    Xo = O.cho_solve_upper(sla.cholesky(A, lower=False), B)
+    assert relnorm(X, Xo) < 1e-11
+
+
+@pytest.mark.parametrize("n", [100, 300, 513])
+def test_potri_and_trsm(n):
+    ctx = G.Context(0)
+    A = _spd(n, seed=9)
+    dA, info = _dev_potrf(ctx, A)
+    dK = ctx.empty(n, n)
+    rc = G._lib.lib.gpr_potri_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                   ctypes.c_void_p(dK.data_ptr()), n)
+    assert rc == 0
+    Kinv = ctx.host(dK)
+    assert relnorm(Kinv, np.linalg.inv(A)) < 1e-11
+    assert np.array_equal(Kinv, Kinv.T)
+    # trsm: B <- U^{-T} B
+    B = np.random.default_rng(2).random((n, 37))
+    dB = ctx.colmajor(B)
+    rc = G._lib.lib.gpr_trsm_upper_trans(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                        ctypes.c_void_p(dB.data_ptr()), 37, n)
+    assert rc == 0
+    U = sla.cholesky(A, lower=False)
+    assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11
+
+
+# ---------------------------------------------------------------------------------------
+# a8/a9 MLL value and gradient  (test/test_loss.jl)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [10, 20, 100])
+def test_mll_closed_form_diagonal(n):
+    """test/test_loss.jl:1-11: K = Diagonal(x) -> MLL = 0.5(sum y^2/x + sum log x + n log 2pi)."""
+    ctx = G.Context(0)
+    rng = np.random.default_rng(n)
+    xv, y = rng.random(n) + 0.1, rng.random(n)
+    MLE = 0.5 * (np.dot(y, y / xv) + np.sum(np.log(xv)) + n * np.log(2 * np.pi))
+    dA, info = _dev_potrf(ctx, np.diag(xv))
+    dy = ctx.colmajor(y)
+    da = ctx.colmajor(y.copy())
+    assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                      ctypes.c_void_p(da.data_ptr()), 1, n) == 0
+    out = ctypes.c_double()
+    assert G._lib.lib.gpr_mll(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                              ctypes.c_void_p(dy.data_ptr()), ctypes.c_void_p(da.data_ptr()),
+                              ctypes.byref(out)) == 0
+    assert out.value == pytest.approx(MLE, rel=1e-13)
+
+
+@pytest.mark.parametrize("n,dim", [(10, 2), (20, 5), (100, 2), (100, 5), (333, 3)])
+def test_mll_and_grad(n, dim):
+    """test/test_loss.jl:22-56: loss, cache contents, per-hp grads vs FD (rtol 1e-3) and
+    vs the oracle (rtol 1e-8 relative to the gradient scale)."""
+    rng = np.random.default_rng(n + dim)
+    x = rng.random((dim, n))
+    y = np.sum(np.sin(x), axis=0)
+    kinds = [SE, WN]
+    hp = np.r_[1.0, rng.uniform(0.5, 2.0, dim), 0.3]
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    L = G.loss(G.MarginalLikelihood(), hp, md)
+    assert L == pytest.approx(O.mll(kinds, hp, x, y), rel=1e-10)
+    tc = G.MllGradCache(md)
+    G.update_cache_(tc, hp, md)
+    ctx = md.ctx
+    U = sla.cholesky(O.kernel(kinds, hp, x), lower=False)
+    assert relnorm(np.triu(ctx.host(tc.kchol_base)), U) < 1e-11
+    np.testing.assert_allclose(ctx.host(tc.alpha), O.cho_solve_upper(U, y), rtol=1e-9, atol=1e-12)
+    assert relnorm(ctx.host(tc.Kinv), O.kinv_from_upper(U)) < 1e-10
+    g = G.grad(G.MarginalLikelihood(), hp, md)
+    go = O.mll_grad(kinds, hp, x, y)
+    scale = np.max(np.abs(go)) + 1.0
+    np.testing.assert_allclose(g, go, rtol=1e-8, atol=1e-8 * scale)
+    for i in range(len(hp)):
+        hpe = hp.copy()
+        hpe[i] += 1e-6
+        fd = (O.mll(kinds, hpe, x, y) - O.mll(kinds, hp, x, y)) / 1e-6
+        assert g[i] == pytest.approx(fd, rel=1e-3, abs=1e-5)
+
+
+def test_mll_2d_y_train_axis():
+    """test/test_loss.jl:58-97: 2-D y with a train_axis column."""
+    rng = np.random.default_rng(4)
+    dim, n, ne = 3, 80, 5
+    x = rng.random((dim, n))
+    y = np.stack([rng.random() * np.sum(np.sin(x), axis=0) for _ in range(ne)], axis=1)
+    ta = 3
+    hp = np.r_[1.0, [1.2] * dim, 0.2]
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, train_axis=ta)
+    L = G.loss(G.MarginalLikelihood(), hp, md)
+    assert L == pytest.approx(O.mll([SE, WN], hp, x, y[:, ta - 1]), rel=1e-10)
+    g = G.grad(G.MarginalLikelihood(), hp, md)
+    go = O.mll_grad([SE, WN], hp, x, y, train_axis=ta)
+    np.testing.assert_allclose(g, go, rtol=1e-8, atol=1e-8 * (1 + np.abs(go).max()))
+
+
+def test_log_loss_grad_and_composed():
+    rng = np.random.default_rng(8)
+    dim, n = 4, 150
+    x = rng.random((dim, n))
+    y = np.sin(x.sum(0)) ** 2
+    kinds = [SE, SE, WN]
+    hp = np.r_[1.0, [2.0] * dim, 0.5, [0.7] * dim, 0.1]
+    md = G.GPRModel(cov_of(kinds), hp, x, y)
+    tc = G.MllGradCache(md)
+    Gv = np.zeros(len(hp))
+    F = G.log_loss_grad_(G.MarginalLikelihood(), 0.0, Gv, np.log(hp), md, tc)
+    assert F == pytest.approx(O.mll(kinds, hp, x, y), rel=1e-10)
+    go = O.mll_grad(kinds, hp, x, y, log_scale=True)
+    np.testing.assert_allclose(Gv, go, rtol=1e-8, atol=1e-8 * (1 + np.abs(go).max()))
+    assert isinstance(G.islog(G.MarginalLikelihood(), md), G.LogScale)
+
+
+# ---------------------------------------------------------------------------------------
+# a10/a11 posterior  (test/test_models.jl)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["SE", "SE+WN", "SE+SE", "SE+SE+WN"])
+@pytest.mark.parametrize("n,npred,dim", [(100, 100, 1), (200, 500, 2), (500, 200, 5), (333, 77, 8)])
+def test_predict_vs_oracle(name, n, npred, dim):
+    kinds = KSETS[name]
+    x, y, xp = O.synthetic(dim, n, npred, seed_train=n, seed_test=npred)
+    hp = O.default_hp(kinds, dim, noise=0.05)
+    md = G.GPRModel(cov_of(kinds), hp, x, y)
+    mu, var = G.predict(md, xp, diagonal_var=True)
+    mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+    np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-10)
+    mu2, S = G.predict(md, xp, diagonal_var=False)
+    _, S_o = O.predict(kinds, hp, x, y, xp, diagonal_var=False)
+    np.testing.assert_allclose(mu2, mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(S, S_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(G.predict_mean(md, xp), mu_o, rtol=1e-8, atol=1e-10)
+
+
+def test_predict_interpolation_and_diag_vs_full():
+    """test/test_models.jl:17-48.  The reference draws hp at random; the interpolation KAT is
+    only meaningful where K is well conditioned, so length-scale multipliers are chosen per
+    dimension (for d=1 the points are a jittered grid: uniform draws can nearly coincide)."""
+    rng = np.random.default_rng(12)
+    for n, npred, dim, l in [(100, 100, 1, 40.0), (200, 200, 2, 14.0), (500, 100, 5, 5.0)]:
+        x, xp = rng.random((dim, n)), rng.random((dim, npred))
+        if dim == 1:
+            x = (np.arange(n) + 0.5 * rng.random(n))[None, :] / n
+        y = np.sin(x.sum(0)) ** 2
+        hp2 = np.r_[1.0, [l] * dim, 0.8, [1.25 * l] * dim]
+        md2 = G.GPRModel(G.SquaredExp() + G.SquaredExp(), hp2, x, y)
+        mu2 = G.predict_mean(md2, x)  # Julia `≈` on arrays is normwise
+        assert np.linalg.norm(mu2 - y) <= 1e-7 * np.linalg.norm(y)
+        _, S = G.predict(md2, x)
+        assert np.abs(S).max() <= 1e-7
+        md3 = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), np.r_[1.0, [l] * dim, 1e-5], x, y)
+        assert np.linalg.norm(G.predict_mean(md3, x) - y) <= 1e-3 * np.linalg.norm(y)
+        _, S3 = G.predict(md3, x)
+        assert np.abs(S3).max() <= 1e-3
+        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), rng.random(dim + 2) + 0.5, x, y)
+        _, Sf = G.predict(md, xp)
+        _, Sd = G.predict(md, xp, diagonal_var=True)
+        np.testing.assert_allclose(np.diag(Sf), Sd, atol=1e-5)
+
+
+def test_predict_multi_output_y():
+    rng = np.random.default_rng(21)
+    dim, n, ne, npred = 3, 150, 4, 60
+    x, xp = rng.random((dim, n)), rng.random((dim, npred))
+    y = np.stack([np.sin(x.sum(0) * (k + 1)) for k in range(ne)], axis=1)
+    kinds = [SE, WN]
+    hp = O.default_hp(kinds, dim)
+    md = G.GPRModel(cov_of(kinds), hp, x, y)
+    mu = G.predict_mean(md, xp)
+    K = O.kernel(kinds, hp, x)
+    U = O.chol_upper(K)
+    mu_o = O.kernel(kinds, hp, xp, x) @ O.cho_solve_upper(U, y)
+    np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+
+
+# ---------------------------------------------------------------------------------------
+# a12-a15 split kernel  (test/test_split_kernel.jl)
+# ---------------------------------------------------------------------------------------
+def test_split_factors_and_identity():
+    rng = np.random.default_rng(13)
+    for dim, n in [(2, 100), (3, 26), (5, 200)]:
+        x, xe, xq = rng.random((dim, n)), rng.random((dim, n + 17)), rng.random((dim, n - 9))
+        kinds = [SE, WN, SE]
+        hp = rng.random(2 * dim + 3)
+        cm = G.Cmap("+", xe, xq)
+        Ao, Bo, Co = O.split_factors(kinds, hp, x, xe, xq)
+        for part in (0, 1):
+            A, B, C = G.split_factors(cov_of(kinds), hp, x, cm, part)
+            np.testing.assert_allclose(A, Ao[:, :, part], rtol=1e-13)
+            np.testing.assert_allclose(B, Bo[:, :, part], rtol=1e-13)
+            np.testing.assert_allclose(C, Co[:, :, part], rtol=1e-13)
+        # SplitCovar identity KK[idx, s] = sum_k A B C  (test/test_split_kernel.jl:36-44)
+        KK = O.kernel(kinds, hp, cm.points(), x)
+        ne, nq = xe.shape[1], xq.shape[1]
+        Ksplit = np.einsum("eqk,esk,sqk->eqs", Ao, Bo, Co).reshape(ne * nq, n, order="F")
+        np.testing.assert_allclose(Ksplit, KK, rtol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["SE", "SE+WN", "SE+SE", "SE+SE+WN"])
+@pytest.mark.parametrize("dim,n,e,q", [(1, 100, 10, 10), (2, 200, 20, 30), (5, 500, 50, 10)])
+def test_split_predict_reference_identities(name, dim, n, e, q):
+    """test/test_split_kernel.jl:49-77 with the reference's random hp: split mean == direct
+    mean on xeq[:, :]; the first 3q variance entries equal the direct variance on
+    Cmap(+, xq, xe) (e-major layout), entry 3q+1 does not (var_range = 1:3)."""
+    kinds = KSETS[name]
+    rng = np.random.default_rng(dim * 1000 + n + e + q)
+    x, xe, xq = rng.random((dim, n)), rng.random((dim, e)), rng.random((dim, q))
+    y = np.sin(x.sum(0)) ** 2
+    hp = rng.random(sum(O.dim_hp(k, dim) for k in kinds)) * 0.5 + 0.5
+    md = G.GPRModel(cov_of(kinds), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    yps, varps = G.predict(md, cm, diagonal_var=True)
+    yp, _ = G.predict(md, cm.points(), diagonal_var=True)
+    np.testing.assert_allclose(yps.reshape(-1, order="F"), yp, rtol=1e-7, atol=1e-9)
+    xpt = G.Cmap("+", xq, xe).points()
+    _, varpt = G.predict(md, xpt, diagonal_var=True)
+    np.testing.assert_allclose(varps[:3 * q], varpt[:3 * q], rtol=1e-5)
+    assert not np.allclose(varps[:3 * q + 1], varpt[:3 * q + 1], rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["SE", "SE+WN", "SE+SE", "SE+SE+WN"])
+@pytest.mark.parametrize("dim,n,e,q", [(4, 200, 20, 30), (5, 500, 50, 10), (8, 640, 33, 17)])
+def test_split_predict_vs_oracle(name, dim, n, e, q):
+    """Split mean/var vs the oracle at rtol 1e-8 on well-posed hp (SURVEY 8d defaults)."""
+    kinds = KSETS[name]
+    rng = np.random.default_rng(dim * 7 + n + e + q)
+    x, xe, xq = rng.random((dim, n)), 0.5 * rng.random((dim, e)), 0.5 * rng.random((dim, q))
+    y = np.sin(x.sum(0)) ** 2
+    hp = O.default_hp(kinds, dim, noise=0.05)
+    md = G.GPRModel(cov_of(kinds), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    yps, varps = G.predict(md, cm, diagonal_var=True)
+    mu_o, var_o = O.split_predict(kinds, hp, x, y, xe, xq)
+    np.testing.assert_allclose(yps, mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(varps, var_o, rtol=1e-8, atol=1e-10)
+
+
+def test_split_predict_full_var_range_and_rows():
+    """var_range = all rows equals the direct diagonal variance; a row-range call writes only
+    its rows (the multi-GPU shard contract)."""
+    rng = np.random.default_rng(99)
+    dim, n, e, q = 3, 300, 12, 40
+    x, xe, xq = rng.random((dim, n)), rng.random((dim, e)), rng.random((dim, q))
+    y = np.sin(x.sum(0)) ** 2
+    kinds = [SE, WN]
+    hp = O.default_hp(kinds, dim)
+    md = G.GPRModel(cov_of(kinds), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    mu, var = G.predict(md, cm, diagonal_var=True, var_range=(1, e))
+    mu_o, var_o = O.split_predict(kinds, hp, x, y, xe, xq, var_range=(1, e))
+    np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-10)
+    # shard rows [4, 9)
+    ctx = md.ctx
+    pc = G.GPRSplitPredictCache(md, e, q, (1, e))
+    from gpr_amd.core import _update_predict_cache, pc_adapter, split_predict_
+    _update_predict_cache(pc_adapter(pc), md)
+    dmu, dvar = ctx.zeros(q, e), ctx.zeros(e * q)
+    split_predict_(md, cm, pc, dmu, dvar, 4, 9)
+    m2, v2 = ctx.host(dmu), ctx.host(dvar)
+    np.testing.assert_allclose(m2[4:9], mu_o[4:9], rtol=1e-8, atol=1e-10)
+    assert np.all(m2[:4] == 0) and np.all(m2[9:] == 0)
+    np.testing.assert_allclose(v2[4 * q:9 * q], var_o[4 * q:9 * q], rtol=1e-8, atol=1e-10)
+    assert np.all(v2[:4 * q] == 0) and np.all(v2[9 * q:] == 0)

@@ -40,7 +40,11 @@ struct gpr_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   std::string err;
-  int nb = 128;  // panel width of the blocked factorisations
+  int nb = 128;   // inner panel width (diag blocks, in-place panel GEMMs)
+  int nb2 = 512;  // outer panel width = K of the big trailing updates (multiple of nb)
+  hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
+  hipStream_t stream2 = nullptr;  // lookahead panel stream
+  std::vector<hipEvent_t> sync_events;
 
   // cached inverses of the diagonal blocks of the last factor: winv[b] = U_bb^{-1}
   // (nb x nb, column-major, strictly-lower part zero), one slot per block.
@@ -98,6 +102,7 @@ struct TimerScope {
   gpr_ctx* ctx;
   TimedLaunch tl;
   bool on;
+  hipStream_t st;
   TimerScope(gpr_ctx* c, int cls, double flops);
   ~TimerScope();
 };
@@ -114,7 +119,8 @@ struct GemmArgs {
   double* C; int ldc;
   int M, N, K;
   double alpha, beta;
-  int upper;              // only tiles/elements with m <= n (SYRK upper)
+  int upper;              // grid over upper tiles only (M == N) + element mask m <= n
+  int mask_upper;         // element mask m <= n on a general grid (local coordinates)
   int kfrom_n;            // tile's K loop starts at its n0 (triangular factor, Z^T Z)
   int kmax_from_n;        // tile's K loop ends at min(K, n0+TN) (lower-triangular RHS)
   const double* qscale;   // optional per-k scale of Q (diag(wt) C)

@@ -20,6 +20,8 @@
 // doubles), next stage prefetched into registers while the current stage's 64 MFMAs per
 // wave run; one barrier per stage.  A K=16 stage is 64 MFMAs x ~64 cycles per wave, so
 // global latency is fully hidden at 2 workgroups per CU.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -29,7 +31,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 struct GemmK {
   GemmArgs g;
-  int tiles_m;
+  int tiles_m, tiles_n;
+  int gm, gn;           // super-tile edges (tiles)
+  int xcd_remap;
+  int super_m;          // super-tiles along m (general grid)
 };
 
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
@@ -39,18 +44,30 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
   __shared__ double Qs[2][TN * LDT];
   __shared__ double red[2][TN];
 
-  int tm, tn;
-  if (g.upper) {
-    const int bid = blockIdx.x;
-    int bj = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
-    while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
-    while (bj * (bj + 1) / 2 > bid) --bj;
-    tn = bj;
-    tm = bid - bj * (bj + 1) / 2;
+  // XCD-aware, super-tile-grouped tile order.  Blocks b and b+8 share an XCD (round-robin
+  // dispatch), so the bijective remap hands each XCD a contiguous range of logical ids;
+  // logical ids walk GxG super-tiles, so the P/Q panels of the ~64 tiles an XCD has in
+  // flight (2G panels of 128 x K) stay in its 4 MB L2.  Placement only affects speed.
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int L = a.xcd_remap ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3)
+                            : bid;
+  const int Gm = a.gm, Gn = a.gn;
+  const int sidx = L / (Gm * Gn), wl = L % (Gm * Gn);
+  int SI, SJ;
+  if (g.upper) {  // upper super-tiles SI <= SJ, triangular order
+    int sj = (int)((sqrt(8.0 * sidx + 1.0) - 1.0) * 0.5);
+    while ((sj + 1) * (sj + 2) / 2 <= sidx) ++sj;
+    while (sj * (sj + 1) / 2 > sidx) --sj;
+    SJ = sj;
+    SI = sidx - sj * (sj + 1) / 2;
   } else {
-    tm = blockIdx.x % a.tiles_m;
-    tn = blockIdx.x / a.tiles_m;
+    SI = sidx % a.super_m;
+    SJ = sidx / a.super_m;
   }
+  const int tm = SI * Gm + (wl % Gm), tn = SJ * Gn + (wl / Gm);
+  if (tm >= a.tiles_m || tn >= a.tiles_n || (g.upper && tm > tn)) return;
   const int m0 = tm * TM, n0 = tn * TN;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
@@ -120,7 +137,28 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
     __syncthreads();
   }
 
-  // ---- epilogue ----
+  // ---- epilogue: all loads first (C, E), then all stores -- interleaving them through
+  // possibly-aliasing pointers would serialise one HBM round trip per element.
+  double* __restrict__ Cp = g.C;
+  const double* __restrict__ Ep = g.E;
+  const bool has_beta = g.beta != 0.0;
+  const bool has_e = Ep != nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wn * 64 + i * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+        const bool in = m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n);
+        double v = acc[i][j][r];
+        if (has_e) v = v * (in ? Ep[(size_t)m + (size_t)n * g.lde] : 0.0);
+        v = g.alpha * v;
+        if (has_beta) v = v + g.beta * (in ? Cp[(size_t)m + (size_t)n * g.ldc] : 0.0);
+        acc[i][j][r] = v;
+      }
+    }
   const bool do_norm = g.norm_out != nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -131,13 +169,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wm * 64 + j * 16 + (lane & 15);
-        if (m < g.M && n < g.N && (!g.upper || m <= n)) {
-          const size_t ci = (size_t)m + (size_t)n * g.ldc;
-          double v = acc[i][j][r];
-          if (g.E) v = v * g.E[(size_t)m + (size_t)n * g.lde];
-          v = g.alpha * v;
-          if (g.beta != 0.0) v = v + g.beta * g.C[ci];
-          g.C[ci] = v;
+        if (m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n)) {
+          const double v = acc[i][j][r];
+          Cp[(size_t)m + (size_t)n * g.ldc] = v;
           nsum = fma(v, v, nsum);
         }
       }
@@ -167,20 +201,29 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   GemmK a;
   a.g = g;
   a.tiles_m = (g.M + TM - 1) / TM;
-  const long long tiles_n = (g.N + TN - 1) / TN;
+  a.tiles_n = (g.N + TN - 1) / TN;
+  static const int genv = getenv("GPR_GEMM_GROUP") ? atoi(getenv("GPR_GEMM_GROUP")) : 8;
+  static const int xenv = getenv("GPR_GEMM_XCD") ? atoi(getenv("GPR_GEMM_XCD")) : 1;
+  a.xcd_remap = xenv;
+  a.gm = std::max(1, std::min(genv, a.tiles_m));
+  a.gn = std::max(1, std::min(genv, a.tiles_n));
+  if (g.upper) a.gn = a.gm;
+  a.super_m = (a.tiles_m + a.gm - 1) / a.gm;
+  const long long super_n = (a.tiles_n + a.gn - 1) / a.gn;
   long long nblk;
   double flops;
   if (g.upper) {
-    if (a.tiles_m != tiles_n) return set_err(ctx, GPR_E_ARG, "upper gemm needs M == N");
-    nblk = tiles_n * (tiles_n + 1) / 2;
+    if (a.tiles_m != a.tiles_n) return set_err(ctx, GPR_E_ARG, "upper gemm needs M == N");
+    nblk = super_n * (super_n + 1) / 2 * a.gm * a.gn;
     flops = (double)g.M * (g.M + 1) * g.K;  // 2 * M(M+1)/2 * K
     if (g.kfrom_n) flops = (double)g.M * g.M * g.M / 3.0;
   } else {
-    nblk = (long long)a.tiles_m * tiles_n;
+    nblk = (long long)a.super_m * super_n * a.gm * a.gn;
     flops = 2.0 * g.M * (double)g.N * g.K;
+    if (g.mask_upper) flops -= (double)g.M * (g.M - 1) * g.K;  // masked lower corner
   }
   TimerScope ts(ctx, timing_class, flops);
-  gemm_tn_kernel<<<(unsigned)nblk, 256, 0, ctx->stream>>>(a);
+  gemm_tn_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
   LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -1,5 +1,6 @@
 // Context, memory, error and timing plumbing of libgpr_hip.so.
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.hpp"
@@ -52,16 +53,17 @@ static hipEvent_t get_event(gpr_ctx* ctx) {
 
 TimerScope::TimerScope(gpr_ctx* c, int cls, double flops) : ctx(c), on(c->timing) {
   if (!on) return;
+  st = ctx->ls ? ctx->ls : ctx->stream;
   tl.cls = cls;
   tl.flops = flops;
   tl.a = get_event(ctx);
   tl.b = get_event(ctx);
-  hipEventRecord(tl.a, ctx->stream);
+  hipEventRecord(tl.a, st);
 }
 
 TimerScope::~TimerScope() {
   if (!on) return;
-  hipEventRecord(tl.b, ctx->stream);
+  hipEventRecord(tl.b, st);
   ctx->pending.push_back(tl);
 }
 
@@ -137,6 +139,12 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     }
     ctx->own_stream = true;
   }
+  ctx->ls = ctx->stream;
+  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return GPR_E_HIP;
+  }
+  if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
   if (hipMalloc((void**)&ctx->dinfo, 64) != hipSuccess) {
     delete ctx;
     return GPR_E_NOMEM;
@@ -150,6 +158,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   hipStreamSynchronize(ctx->stream);
   drain_timing(ctx);
   for (auto e : ctx->event_pool) hipEventDestroy(e);
+  for (auto e : ctx->sync_events) hipEventDestroy(e);
+  if (ctx->stream2) hipStreamDestroy(ctx->stream2);
   if (ctx->winv) hipFree(ctx->winv);
   if (ctx->dinfo) hipFree(ctx->dinfo);
   if (ctx->dscratch) hipFree(ctx->dscratch);
@@ -199,7 +209,15 @@ int gpr_download(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes) {
 int gpr_set_block(gpr_ctx_t ctx, int nb) {
   if (nb != 64 && nb != 128) return set_err(ctx, GPR_E_ARG, "nb must be 64 or 128 (got %d)", nb);
   ctx->nb = nb;
+  if (ctx->nb2 % nb) ctx->nb2 = 4 * nb;
   ctx->fac_valid = false;
+  return 0;
+}
+
+int gpr_set_outer_block(gpr_ctx_t ctx, int nb2) {
+  if (nb2 < ctx->nb || nb2 % ctx->nb)
+    return set_err(ctx, GPR_E_ARG, "outer block %d must be a multiple of nb=%d", nb2, ctx->nb);
+  ctx->nb2 = nb2;
   return 0;
 }
 

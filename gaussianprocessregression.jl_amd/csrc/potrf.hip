@@ -16,13 +16,37 @@
 
 #include "common.hpp"
 
+#ifdef GPR_DIAG_STAMPS
+// diagnostic build only (tools/gemm_bench): wall-clock stamps of the diag kernel phases
+__device__ unsigned long long g_diag_stamps[16];
+#define STAMP(i)                                                                       \
+  do {                                                                                 \
+    __syncthreads();                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+extern "C" void gpr_debug_diag_stamps(unsigned long long* out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_stamps), sizeof(unsigned long long) * 16);
+}
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int DIAG_THREADS = 512;
 
-// Factor (mode 1) or only invert an existing factor (mode 0) of one diagonal block.
-// mode 1: one launch per panel, blockIdx.x == 0, block at A (lda), size kb, global offset
-//         kglob; mode 0: grid = number of blocks, block b at A + b*nb*(lda+1).
+// Factor (mode 1) or only invert an existing factor (mode 0) of one NB x NB diagonal block.
+// mode 1: one launch per panel, block at A + kglob*(lda+1), size kb = min(NB, n-kglob);
+// mode 0: grid = number of blocks, block b at A + b*NB*(lda+1).
+//
+// Register-owned right-looking algorithm: thread (tr, tc) = (t & 31, t >> 5) owns the
+// elements (tr + 32a, tc + 16b) of the block (upper part), so each of the NB sequential
+// steps is: owners of the pivot row publish it to a double-buffered LDS row, ONE barrier,
+// every thread updates its elements from the broadcast row.  The inverse U^{-1} (needed so
+// the panel TRSM becomes an MFMA GEMM) is built the same way (X U = I, right-looking over
+// columns) with U read from an LDS copy.  Padding beyond kb is the identity.
 template <int NB>
 __global__ __launch_bounds__(DIAG_THREADS) void diag_block_kernel(double* __restrict__ A,
                                                                   size_t lda, int n, int kglob,
@@ -30,10 +54,12 @@ __global__ __launch_bounds__(DIAG_THREADS) void diag_block_kernel(double* __rest
                                                                   double* __restrict__ winv,
                                                                   int mode) {
   constexpr int LD = NB + 1;
+  constexpr int RA = NB / 32, CB = NB / 16;
   __shared__ double S[NB * LD];
-  __shared__ double Sd[NB];
+  __shared__ double buf[2][NB];
   if (*info != 0) return;
   const int tid = threadIdx.x;
+  const int tr = tid & 31, tc = tid >> 5;
   int k0, kb;
   if (mode == 1) {
     k0 = kglob;
@@ -44,72 +70,145 @@ __global__ __launch_bounds__(DIAG_THREADS) void diag_block_kernel(double* __rest
     winv += (size_t)blockIdx.x * NB * NB;
   }
   double* Ab = A + (size_t)k0 + (size_t)k0 * lda;
-  for (int idx = tid; idx < NB * NB; idx += DIAG_THREADS) {
-    const int r = idx % NB, c = idx / NB;
-    double v = (r == c) ? 1.0 : 0.0;
-    if (r < kb && c < kb && r <= c) v = Ab[(size_t)r + (size_t)c * lda];
-    S[r + c * LD] = v;
-  }
-  __syncthreads();
+  STAMP(0);
+  double a[RA][CB];
+#pragma unroll
+  for (int ai = 0; ai < RA; ++ai)
+#pragma unroll
+    for (int bi = 0; bi < CB; ++bi) {
+      const int r = tr + 32 * ai, c = tc + 16 * bi;
+      double v = (r == c) ? 1.0 : 0.0;
+      if (r < kb && c < kb && r <= c) v = Ab[(size_t)r + (size_t)c * lda];
+      a[ai][bi] = v;
+    }
 
+  STAMP(1);
   if (mode == 1) {
     for (int j = 0; j < kb; ++j) {
-      const double ajj = S[j + j * LD];
-      if (!(ajj > 0.0)) {  // also catches NaN (dpotf2: ajj <= 0 .or. disnan(ajj))
+      const int p = j & 1;
+      if (tr == (j & 31)) {  // owners of row j publish it (entries c < j are never read)
+        const int aj = j >> 5;
+#pragma unroll
+        for (int bi = 0; bi < CB; ++bi) {
+          double v = a[0][bi];
+#pragma unroll
+          for (int ai = 1; ai < RA; ++ai) v = (ai == aj) ? a[ai][bi] : v;
+          buf[p][tc + 16 * bi] = v;
+        }
+      }
+      __syncthreads();
+      const double dj = buf[p][j];
+      if (!(dj > 0.0)) {  // also catches NaN (dpotf2: ajj <= 0 .or. disnan(ajj))
         if (tid == 0) *info = kglob + j + 1;
         return;
       }
-      const double ujj = sqrt(ajj);
-      __syncthreads();
-      for (int c = j + tid; c < kb; c += DIAG_THREADS)
-        S[j + c * LD] = (c == j) ? ujj : S[j + c * LD] / ujj;
-      __syncthreads();
-      const int nc = kb - j - 1;
-      for (int idx = tid; idx < nc * nc; idx += DIAG_THREADS) {
-        const int rr = idx % nc, cc = idx / nc;
-        if (rr <= cc) {
-          const int r = j + 1 + rr, c = j + 1 + cc;
-          S[r + c * LD] -= S[j + r * LD] * S[j + c * LD];
+      const double u = sqrt(dj);
+      const double ri = 1.0 / u;
+      double ur[RA], uc[CB];
+#pragma unroll
+      for (int ai = 0; ai < RA; ++ai) {
+        const int r = tr + 32 * ai;
+        const double v = buf[p][r];  // unconditional load, then select (no branch/wait)
+        ur[ai] = (r > j) ? v * ri : 0.0;
+      }
+#pragma unroll
+      for (int bi = 0; bi < CB; ++bi) {
+        const int c = tc + 16 * bi;
+        const double v = buf[p][c];
+        uc[bi] = (c > j) ? v * ri : 0.0;
+      }
+      // ur/uc are zero outside the trailing block, so the rank-1 update is a no-op there
+      // (elements below the diagonal take garbage that is never stored).  Row/column blocks
+      // that are entirely finished (<= j) are skipped with wave-uniform branches.
+#pragma unroll
+      for (int ai = 0; ai < RA; ++ai) {
+        if (32 * ai + 31 < j) continue;
+        const int r = tr + 32 * ai;
+#pragma unroll
+        for (int bi = 0; bi < CB; ++bi) {
+          if (16 * bi + 15 < j) continue;
+          const int c = tc + 16 * bi;
+          const double upd = fma(-ur[ai], uc[bi], a[ai][bi]);
+          if (32 * ai <= j) {  // this row block contains row j: finalise U[j][c]
+            const double rowj = (c == j) ? u : ((c > j) ? uc[bi] : a[ai][bi]);
+            a[ai][bi] = (r == j) ? rowj : upd;
+          } else {
+            a[ai][bi] = upd;
+          }
         }
       }
-      __syncthreads();
     }
   }
 
-  // W = U^{-T} (lower): U^T W = I, row by row; 8 lanes per column, 64 columns per pass.
-  const int sub = tid & 7, colg = tid >> 3;
-  for (int r = 0; r < kb; ++r) {
-    const double urr = S[r + r * LD];
-    for (int c0 = 0; c0 <= r; c0 += DIAG_THREADS / 8) {
-      const int c = c0 + colg;
-      double s = 0.0;
-      if (c <= r) {
-        for (int p = c + sub; p < r; p += 8) {
-          const double wpc = (p == c) ? Sd[c] : S[p + c * LD];
-          s = fma(S[p + r * LD], wpc, s);
-        }
+  STAMP(2);
+  // U (upper) -> LDS copy (and back to global in mode 1)
+#pragma unroll
+  for (int ai = 0; ai < RA; ++ai)
+#pragma unroll
+    for (int bi = 0; bi < CB; ++bi) {
+      const int r = tr + 32 * ai, c = tc + 16 * bi;
+      if (r <= c) {
+        S[r + c * LD] = a[ai][bi];
+        if (mode == 1 && r < kb && c < kb) Ab[(size_t)r + (size_t)c * lda] = a[ai][bi];
       }
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      s += __shfl_xor(s, 4);
-      if (c <= r && sub == 0) {
-        if (c == r)
-          Sd[r] = 1.0 / urr;
-        else
-          S[r + c * LD] = (-s) / urr;
+    }
+  // X = U^{-1}: X U = I, right-looking over columns; X owned like U, starts as I.
+#pragma unroll
+  for (int ai = 0; ai < RA; ++ai)
+#pragma unroll
+    for (int bi = 0; bi < CB; ++bi) a[ai][bi] = (tr + 32 * ai == tc + 16 * bi) ? 1.0 : 0.0;
+  __syncthreads();
+  STAMP(3);
+  for (int r = 0; r < kb; ++r) {
+    const int p = r & 1;
+    const double urr = S[r + r * LD];
+    if (tc == (r & 15)) {  // owners of column r finalise it: X[i][r] /= U[r][r]
+      const int br = r >> 4;
+#pragma unroll
+      for (int ai = 0; ai < RA; ++ai) {
+        double v = a[ai][0];
+#pragma unroll
+        for (int bi = 1; bi < CB; ++bi) v = (bi == br) ? a[ai][bi] : v;
+        const double x = v / urr;
+        const bool fin = (tr + 32 * ai) <= r;
+#pragma unroll
+        for (int bi = 0; bi < CB; ++bi) a[ai][bi] = (bi == br && fin) ? x : a[ai][bi];
+        buf[p][tr + 32 * ai] = x;  // entries i > r are never read
       }
     }
     __syncthreads();
+    double xc[RA], ur[CB];
+#pragma unroll
+    for (int ai = 0; ai < RA; ++ai) {
+      const int i = tr + 32 * ai;
+      const double v = buf[p][i];
+      xc[ai] = (i <= r) ? v : 0.0;
+    }
+#pragma unroll
+    for (int bi = 0; bi < CB; ++bi) {
+      const int jj = tc + 16 * bi;
+      const double v = S[r + jj * LD];
+      ur[bi] = (jj > r) ? v : 0.0;
+    }
+#pragma unroll
+    for (int ai = 0; ai < RA; ++ai) {
+      if (32 * ai > r) continue;            // rows i > r untouched
+#pragma unroll
+      for (int bi = 0; bi < CB; ++bi) {
+        if (16 * bi + 15 <= r) continue;    // columns jj <= r finished
+        a[ai][bi] = fma(-xc[ai], ur[bi], a[ai][bi]);
+      }
+    }
   }
-
-  // write U back (mode 1) and U^{-1}[k][m] = W[m][k] (upper) to the workspace slot
-  for (int idx = tid; idx < NB * NB; idx += DIAG_THREADS) {
-    const int r = idx % NB, c = idx / NB;
-    if (mode == 1 && r < kb && c < kb && r <= c) Ab[(size_t)r + (size_t)c * lda] = S[r + c * LD];
-    double wv = 0.0;
-    if (r < kb && c < kb) wv = (r == c) ? Sd[r] : (r < c ? S[c + r * LD] : 0.0);
-    winv[r + c * NB] = wv;
-  }
+  STAMP(4);
+  // write U^{-1} (upper, zero below, zero outside kb) to the workspace slot
+#pragma unroll
+  for (int ai = 0; ai < RA; ++ai)
+#pragma unroll
+    for (int bi = 0; bi < CB; ++bi) {
+      const int r = tr + 32 * ai, c = tc + 16 * bi;
+      winv[r + c * NB] = (r <= c && r < kb && c < kb) ? a[ai][bi] : 0.0;
+    }
 }
 
 // ---- small-RHS triangular solves (TRSV-like, nrhs <= 16 per launch) --------------------
@@ -191,50 +290,152 @@ int launch_diag(gpr_ctx* ctx, double* A, int lda, int n, int kglob, double* winv
   const int nb = ctx->nb;
   TimerScope ts(ctx, TC_PANEL, 0.0);
   if (nb == 128)
-    diag_block_kernel<128><<<nblocks, DIAG_THREADS, 0, ctx->stream>>>(A, (size_t)lda, n, kglob,
+    diag_block_kernel<128><<<nblocks, DIAG_THREADS, 0, ctx->ls>>>(A, (size_t)lda, n, kglob,
                                                                       ctx->dinfo, winv, mode);
   else
-    diag_block_kernel<64><<<nblocks, DIAG_THREADS, 0, ctx->stream>>>(A, (size_t)lda, n, kglob,
+    diag_block_kernel<64><<<nblocks, DIAG_THREADS, 0, ctx->ls>>>(A, (size_t)lda, n, kglob,
                                                                      ctx->dinfo, winv, mode);
   LAUNCH_CHECK(ctx);
   return 0;
 }
 
-}  // namespace
+hipEvent_t sync_event(gpr_ctx* ctx, size_t i) {
+  while (ctx->sync_events.size() <= i) {
+    hipEvent_t e;
+    hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    ctx->sync_events.push_back(e);
+  }
+  return ctx->sync_events[i];
+}
 
-int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
+// Factor the rows [k, k+kw) of the (already updated) trailing matrix: per inner block j:
+// diag factor+inverse, in-place panel TRSM over all columns >= j+jb (MFMA GEMM with
+// U_jj^{-1}), then the update of the remaining rows of this outer panel (K = nb).
+int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   const int nb = ctx->nb;
-  ctx->fac_valid = false;
-  GPR_TRY(ensure_winv(ctx, n, nb));
-  HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
-  for (int k = 0; k < n; k += nb) {
-    const int kb = std::min(nb, n - k);
-    double* wk = ctx->winv + (size_t)(k / nb) * nb * nb;
-    GPR_TRY(launch_diag(ctx, dA, lda, n, k, wk, 1, 1));
-    const int rest = n - k - kb;
-    if (rest <= 0) break;
-    double* panel = dA + k + (size_t)(k + kb) * lda;
+  for (int j = k; j < k + kw; j += nb) {
+    const int jb = std::min(nb, n - j);
+    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
+    GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
+    if (j + jb >= n) break;
+    double* row = A + j + (size_t)(j + jb) * lda;
     GemmArgs g{};
-    g.P = wk; g.ldp = nb;
-    g.Q = panel; g.ldq = lda;
-    g.C = panel; g.ldc = lda;
-    g.M = kb; g.N = rest; g.K = kb;
+    g.P = wj; g.ldp = nb;
+    g.Q = row; g.ldq = lda;
+    g.C = row; g.ldc = lda;
+    g.M = jb; g.N = n - j - jb; g.K = jb;
     g.alpha = 1.0; g.beta = 0.0;
     g.info = ctx->dinfo;
     GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
-    GemmArgs s{};
-    s.P = panel; s.ldp = lda;
-    s.Q = panel; s.ldq = lda;
-    s.C = dA + (k + kb) + (size_t)(k + kb) * lda; s.ldc = lda;
-    s.M = rest; s.N = rest; s.K = kb;
-    s.alpha = -1.0; s.beta = 1.0;
-    s.upper = 1;
-    s.info = ctx->dinfo;
-    GPR_TRY(launch_gemm_tn(ctx, s, TC_SYRK));
+    if (j + jb < k + kw) {
+      GemmArgs u{};
+      u.P = row; u.ldp = lda;
+      u.Q = row; u.ldq = lda;
+      u.C = A + (j + jb) + (size_t)(j + jb) * lda; u.ldc = lda;
+      u.M = k + kw - j - jb; u.N = n - j - jb; u.K = jb;
+      u.alpha = -1.0; u.beta = 1.0;
+      u.mask_upper = 1;
+      u.info = ctx->dinfo;
+      GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
+    }
   }
+  return 0;
+}
+
+// TRSM panel: X_j = W_j^T B_j for the inner blocks of rows [k, k+kw), each followed by
+// the update of the remaining rows of the outer block (K = nb).
+int trsm_panel(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int ncols, int ldb,
+               double* norm_out, int k, int kw) {
+  const int nb = ctx->nb;
+  for (int j = k; j < k + kw; j += nb) {
+    const int jb = std::min(nb, n - j);
+    GemmArgs g{};
+    g.P = ctx->winv + (size_t)(j / nb) * nb * nb; g.ldp = nb;
+    g.Q = dB + j; g.ldq = ldb;
+    g.C = dB + j; g.ldc = ldb;
+    g.M = jb; g.N = ncols; g.K = jb;
+    g.alpha = 1.0; g.beta = 0.0;
+    g.norm_out = norm_out;
+    GPR_TRY(launch_gemm_tn(ctx, g, TC_TRSM_GEMM));
+    if (j + jb < k + kw) {
+      GemmArgs u{};
+      u.P = dU + j + (size_t)(j + jb) * ldu; u.ldp = ldu;
+      u.Q = dB + j; u.ldq = ldb;
+      u.C = dB + j + jb; u.ldc = ldb;
+      u.M = k + kw - j - jb; u.N = ncols; u.K = jb;
+      u.alpha = -1.0; u.beta = 1.0;
+      GPR_TRY(launch_gemm_tn(ctx, u, TC_TRSM_GEMM));
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+// Two-level right-looking upper Cholesky with depth-1 lookahead.
+//   outer panels P_s = rows [s*nb2, (s+1)*nb2)      (nb2 = K of the big MFMA updates)
+//   stream2 (panel):  wait b_{s-1}; a_s = update of rows P_{s+1} by P_s; factor P_{s+1}
+//   stream  (main):   wait panel_s; b_s = SYRK of rows/cols >= (s+2)*nb2 by P_s
+// so the latency-bound diag/TRSM chain of panel s+1 overlaps the big SYRK b_s.
+int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
+  const int nb = ctx->nb;
+  const int nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
+  ctx->fac_valid = false;
+  GPR_TRY(ensure_winv(ctx, n, nb));
+  hipStream_t s0 = ctx->stream, s1 = ctx->stream2;
+  HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), s0));
+  size_t ev = 0;
+  hipEvent_t e0 = sync_event(ctx, ev++);
+  HIP_TRY(ctx, hipEventRecord(e0, s0));
+  HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
+  ctx->ls = s1;
+  int rc = factor_panel(ctx, dA, n, lda, 0, std::min(nb2, n));
+  hipEvent_t ev_p = sync_event(ctx, ev++);
+  hipEvent_t ev_b = nullptr;
+  if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
+  for (int k = 0; !rc && k + nb2 < n; k += nb2) {
+    const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
+    // ---- panel stream: a_s (rows P_{s+1} by P_s), then factor panel s+1
+    ctx->ls = s1;
+    if (ev_b && hipStreamWaitEvent(s1, ev_b, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    GemmArgs a{};
+    a.P = dA + k + (size_t)kend * lda; a.ldp = lda;
+    a.Q = a.P; a.ldq = lda;
+    a.C = dA + kend + (size_t)kend * lda; a.ldc = lda;
+    a.M = w2; a.N = n - kend; a.K = nb2;
+    a.alpha = -1.0; a.beta = 1.0;
+    a.mask_upper = 1;
+    a.info = ctx->dinfo;
+    if ((rc = launch_gemm_tn(ctx, a, TC_PANEL))) break;
+    if ((rc = factor_panel(ctx, dA, n, lda, kend, w2))) break;
+    hipEvent_t ev_p_next = sync_event(ctx, ev++);
+    if (hipEventRecord(ev_p_next, s1) != hipSuccess) { rc = GPR_E_HIP; break; }
+    // ---- main stream: b_s
+    ctx->ls = s0;
+    if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    if (rest0 < n) {
+      GemmArgs b{};
+      b.P = dA + k + (size_t)rest0 * lda; b.ldp = lda;
+      b.Q = b.P; b.ldq = lda;
+      b.C = dA + rest0 + (size_t)rest0 * lda; b.ldc = lda;
+      b.M = n - rest0; b.N = n - rest0; b.K = nb2;
+      b.alpha = -1.0; b.beta = 1.0;
+      b.upper = 1;
+      b.info = ctx->dinfo;
+      if ((rc = launch_gemm_tn(ctx, b, TC_SYRK))) break;
+    }
+    ev_b = sync_event(ctx, ev++);
+    if (hipEventRecord(ev_b, s0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    ev_p = ev_p_next;
+  }
+  ctx->ls = s0;
+  hipEvent_t ej = sync_event(ctx, ev++);  // join the panel stream into the main stream
+  HIP_TRY(ctx, hipEventRecord(ej, s1));
+  HIP_TRY(ctx, hipStreamWaitEvent(s0, ej, 0));
+  if (rc) return rc;
   int hinfo = 0;
-  HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, s0));
+  HIP_TRY(ctx, hipStreamSynchronize(s0));
   if (info) *info = hinfo;
   if (hinfo == 0) {
     ctx->fac_valid = true;
@@ -263,36 +464,62 @@ int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
   return 0;
 }
 
-// B <- U^{-T} B (Uᵀ X = B), GEMM-based (any nrhs).  norm_out: optional per-column
-// accumulation norm_out[c] -= ||X[:, c]||^2.  lower_rhs: B is lower-triangular
-// (identity RHS) -> step b only touches columns [0, (b+1) nb).
+// B <- U^{-T} B (U^T X = B), GEMM-based (any nrhs), two-level with the same lookahead
+// structure as potrf_core.  norm_out: optional norm_out[c] -= ||X[:, c]||^2 (fused in the
+// panel GEMM epilogue).  lower_rhs: B is lower-triangular (identity RHS) -> outer block s
+// only touches columns [0, (s+1) nb2).
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs) {
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   const int nb = ctx->nb;
-  for (int k = 0; k < n; k += nb) {
-    const int kb = std::min(nb, n - k);
-    const int ncols = lower_rhs ? std::min(nrhs, k + kb) : nrhs;
-    double* wk = ctx->winv + (size_t)(k / nb) * nb * nb;
-    GemmArgs g{};
-    g.P = wk; g.ldp = nb;
-    g.Q = dB + k; g.ldq = ldb;
-    g.C = dB + k; g.ldc = ldb;
-    g.M = kb; g.N = ncols; g.K = kb;
-    g.alpha = 1.0; g.beta = 0.0;
-    g.norm_out = norm_out;
-    GPR_TRY(launch_gemm_tn(ctx, g, TC_TRSM_GEMM));
-    const int rest = n - k - kb;
-    if (rest <= 0) break;
-    GemmArgs s{};
-    s.P = dU + k + (size_t)(k + kb) * ldu; s.ldp = ldu;
-    s.Q = dB + k; s.ldq = ldb;
-    s.C = dB + k + kb; s.ldc = ldb;
-    s.M = rest; s.N = ncols; s.K = kb;
-    s.alpha = -1.0; s.beta = 1.0;
-    GPR_TRY(launch_gemm_tn(ctx, s, TC_TRSM_GEMM));
+  const int nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
+  hipStream_t s0 = ctx->stream, s1 = ctx->stream2;
+  size_t ev = 0;
+  hipEvent_t e0 = sync_event(ctx, ev++);
+  HIP_TRY(ctx, hipEventRecord(e0, s0));
+  HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
+  auto cols = [&](int kend) { return lower_rhs ? std::min(nrhs, kend) : nrhs; };
+  ctx->ls = s1;
+  const int w0 = std::min(nb2, n);
+  int rc = trsm_panel(ctx, dU, n, ldu, dB, cols(w0), ldb, norm_out, 0, w0);
+  hipEvent_t ev_p = sync_event(ctx, ev++);
+  hipEvent_t ev_b = nullptr;
+  if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
+  for (int k = 0; !rc && k + nb2 < n; k += nb2) {
+    const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
+    const int nc = cols(kend);
+    ctx->ls = s1;
+    if (ev_b && hipStreamWaitEvent(s1, ev_b, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    GemmArgs a{};
+    a.P = dU + k + (size_t)kend * ldu; a.ldp = ldu;
+    a.Q = dB + k; a.ldq = ldb;
+    a.C = dB + kend; a.ldc = ldb;
+    a.M = w2; a.N = nc; a.K = nb2;
+    a.alpha = -1.0; a.beta = 1.0;
+    if ((rc = launch_gemm_tn(ctx, a, TC_TRSM_GEMM))) break;
+    if ((rc = trsm_panel(ctx, dU, n, ldu, dB, cols(rest0), ldb, norm_out, kend, w2))) break;
+    hipEvent_t ev_p_next = sync_event(ctx, ev++);
+    if (hipEventRecord(ev_p_next, s1) != hipSuccess) { rc = GPR_E_HIP; break; }
+    ctx->ls = s0;
+    if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    if (rest0 < n) {
+      GemmArgs b{};
+      b.P = dU + k + (size_t)rest0 * ldu; b.ldp = ldu;
+      b.Q = dB + k; b.ldq = ldb;
+      b.C = dB + rest0; b.ldc = ldb;
+      b.M = n - rest0; b.N = nc; b.K = nb2;
+      b.alpha = -1.0; b.beta = 1.0;
+      if ((rc = launch_gemm_tn(ctx, b, TC_TRSM_GEMM))) break;
+    }
+    ev_b = sync_event(ctx, ev++);
+    if (hipEventRecord(ev_b, s0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    ev_p = ev_p_next;
   }
-  return 0;
+  ctx->ls = s0;
+  hipEvent_t ej = sync_event(ctx, ev++);
+  HIP_TRY(ctx, hipEventRecord(ej, s1));
+  HIP_TRY(ctx, hipStreamWaitEvent(s0, ej, 0));
+  return rc;
 }
 
 // B <- K^{-1} B with small nrhs (dpotrs): blocked forward U^T z = b, backward U x = z.

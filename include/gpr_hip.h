@@ -68,8 +68,10 @@ int gpr_malloc(gpr_ctx_t ctx, size_t bytes, void** dptr);
 int gpr_free(gpr_ctx_t ctx, void* dptr);
 int gpr_upload(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes);   /* sync H2D */
 int gpr_download(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes); /* sync D2H */
-/* Panel width of the blocked factorisations (default 128).  Must be a multiple of 64. */
+/* Inner panel width of the blocked factorisations: 64 or 128 (default 128). */
 int gpr_set_block(gpr_ctx_t ctx, int nb);
+/* Outer panel width = K of the big MFMA trailing updates (default 512, multiple of nb). */
+int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
 /* Per-kernel-class timing with HIP events on the context stream (bench instrumentation).
  * class: 0 K-assembly, 1 POTRF trailing update (SYRK), 2 POTRF panel (diag+TRSM),
  *        3 TRSM trailing GEMM, 4 other.  Returns accumulated ms, launch count, flops. */

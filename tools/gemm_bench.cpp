@@ -1,0 +1,82 @@
+// Standalone timing of launch_gemm_tn (SYRK / TRSM-update shapes) and potrf.
+// Build: make -C gaussianprocessregression.jl_amd/csrc bench   (links the library objects)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../gaussianprocessregression.jl_amd/csrc/common.hpp"
+
+__global__ void init_kernel(double* p, size_t n, unsigned seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    unsigned h = (unsigned)(i * 2654435761u) ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
+    p[i] = (h & 0xffffff) / 16777216.0 - 0.5;
+  }
+}
+
+extern "C" void gpr_debug_diag_stamps(unsigned long long* out);
+
+int main(int argc, char** argv) {
+  int N = argc > 1 ? atoi(argv[1]) : 16384;
+  int K = argc > 2 ? atoi(argv[2]) : 128;
+  int mode = argc > 3 ? atoi(argv[3]) : 0;  // 0 syrk upper, 1 general (M=N=N, K), 2 potrf
+  gpr_ctx_t ctx;
+  gpr_ctx_create(0, nullptr, &ctx);
+  hipStream_t s = (hipStream_t)gpr_ctx_stream(ctx);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  if (mode == 2) {
+    // SPD matrix: K = kernel(SE+WN) of random points via the public API
+    int d = 8;
+    double *X, *A;
+    hipMalloc(&X, sizeof(double) * d * N);
+    hipMalloc(&A, sizeof(double) * (size_t)N * N);
+    init_kernel<<<1024, 256, 0, s>>>(X, (size_t)d * N, 7);
+    int kinds[3] = {GPR_SE, GPR_SE, GPR_WN};
+    std::vector<double> hp(2 * (d + 1) + 1, 3.0);
+    hp[0] = 1.0; hp[d + 1] = 1.0; hp[2 * (d + 1)] = 0.1;
+    for (int rep = 0; rep < 3; ++rep) {
+      gpr_kernel(ctx, kinds, 3, hp.data(), d, X, N, nullptr, N, 1, 1e-8, A, N);
+      gpr_timing_reset(ctx);
+      gpr_timing_enable(ctx, rep == 2);
+      hipEventRecord(e0, s);
+      int info = 0;
+      gpr_potrf_upper(ctx, A, N, N, &info);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+      float ms; hipEventElapsedTime(&ms, e0, e1);
+      printf("potrf N=%d: %.2f ms  %.2f TFLOP/s info=%d\n", N, ms, (double)N * N * N / 3 / ms / 1e9, info);
+    }
+    {
+      unsigned long long st[16];
+      gpr_debug_diag_stamps(st);
+      printf("last diag stamps (us from start, 100 MHz clock): load %.2f factor %.2f copy %.2f inverse %.2f\n",
+             (st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0, (st[4] - st[3]) / 100.0);
+    }
+    const char* nm[5] = {"kbuild", "syrk", "panel", "trsm", "other"};
+    for (int c = 0; c < 5; ++c) {
+      double ms, fl; long long ln;
+      gpr_timing_get(ctx, c, &ms, &ln, &fl);
+      if (ln) printf("  %-6s %8.2f ms %5lld launches %7.2f TF\n", nm[c], ms, ln, fl / ms / 1e9);
+    }
+    return 0;
+  }
+  double *P, *C;
+  hipMalloc(&P, sizeof(double) * (size_t)K * N);
+  hipMalloc(&C, sizeof(double) * (size_t)N * N);
+  init_kernel<<<1024, 256, 0, s>>>(P, (size_t)K * N, 1);
+  init_kernel<<<1024, 256, 0, s>>>(C, (size_t)N * N, 2);
+  GemmArgs g{};
+  g.P = P; g.ldp = K; g.Q = P; g.ldq = K; g.C = C; g.ldc = N;
+  g.M = N; g.N = N; g.K = K; g.alpha = -1.0; g.beta = 1.0; g.upper = (mode == 0);
+  double flops = mode == 0 ? (double)N * (N + 1) * K : 2.0 * N * N * K;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEventRecord(e0, s);
+    launch_gemm_tn(ctx, g, TC_OTHER);
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    if (rep >= 2) printf("gemm mode=%d N=%d K=%d: %.3f ms  %.2f TFLOP/s\n", mode, N, K, ms, flops / ms / 1e9);
+  }
+  return 0;
+}

@@ -41,10 +41,15 @@ struct gpr_ctx {
   bool own_stream = false;
   std::string err;
   int nb = 128;   // inner panel width (diag blocks, in-place panel GEMMs)
-  int nb2 = 512;  // outer panel width = K of the big trailing updates (multiple of nb)
+  int nb2 = 768;  // outer panel width = K of the big trailing updates (multiple of nb)
   hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
-  hipStream_t stream2 = nullptr;  // lookahead panel stream
+  hipStream_t stream2 = nullptr;  // lookahead panel stream (GEMMs of the panel chain)
+  hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
+  hipStream_t smain = nullptr;    // big trailing updates: CU mask = all but the reserved CUs
+  int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
+  int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   std::vector<hipEvent_t> sync_events;
+  size_t ev_next = 0;
 
   // cached inverses of the diagonal blocks of the last factor: winv[b] = U_bb^{-1}
   // (nb x nb, column-major, strictly-lower part zero), one slot per block.
@@ -120,13 +125,15 @@ struct GemmArgs {
   int M, N, K;
   double alpha, beta;
   int upper;              // grid over upper tiles only (M == N) + element mask m <= n
-  int mask_upper;         // element mask m <= n on a general grid (local coordinates)
+  int mask_upper;         // element mask m <= n + mask_off on a general grid
+  int mask_off;           // column offset of C relative to its row origin (mask_upper)
   int kfrom_n;            // tile's K loop starts at its n0 (triangular factor, Z^T Z)
   int kmax_from_n;        // tile's K loop ends at min(K, n0+TN) (lower-triangular RHS)
   const double* qscale;   // optional per-k scale of Q (diag(wt) C)
   const double* E; int lde;  // optional Hadamard factor: C = beta*C + alpha*acc*E
   double* norm_out;       // optional: norm_out[n] -= sum_m (result)^2 (needs M <= tile)
   const int* info;        // optional: skip when *info != 0
+  int occ1;               // launch at one workgroup per CU (lookahead co-residence)
 };
 int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class);
 

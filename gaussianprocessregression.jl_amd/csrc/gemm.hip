@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
   const int tm = SI * Gm + (wl % Gm), tn = SJ * Gn + (wl / Gm);
   if (tm >= a.tiles_m || tn >= a.tiles_n || (g.upper && tm > tn)) return;
   const int m0 = tm * TM, n0 = tn * TN;
+  if (g.mask_upper && m0 > n0 + TN - 1 + g.mask_off) return;  // tile entirely below diagonal
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
 
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wm * 64 + j * 16 + (lane & 15);
-        const bool in = m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n);
+        const bool in = m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n + g.mask_off);
         double v = acc[i][j][r];
         if (has_e) v = v * (in ? Ep[(size_t)m + (size_t)n * g.lde] : 0.0);
         v = g.alpha * v;
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wm * 64 + j * 16 + (lane & 15);
-        if (m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n)) {
+        if (m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n + g.mask_off)) {
           const double v = acc[i][j][r];
           Cp[(size_t)m + (size_t)n * g.ldc] = v;
           nsum = fma(v, v, nsum);
@@ -220,10 +221,18 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   } else {
     nblk = (long long)a.super_m * super_n * a.gm * a.gn;
     flops = 2.0 * g.M * (double)g.N * g.K;
-    if (g.mask_upper) flops -= (double)g.M * (g.M - 1) * g.K;  // masked lower corner
+    if (g.mask_upper) {  // exclude the masked corner rows m > n + mask_off
+      const double rows_below = std::max(0.0, (double)g.M - g.mask_off);
+      const double cut = std::min(rows_below, (double)g.N);
+      flops = 2.0 * g.K * ((double)g.M * g.N - (cut * (cut - 1) / 2.0 + std::max(0.0, rows_below - g.N) * g.N));
+    }
   }
   TimerScope ts(ctx, timing_class, flops);
-  gemm_tn_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
+  // g.occ1: reserve LDS so only ONE such workgroup fits per CU, leaving the other half of
+  // every CU to a concurrent (lookahead) stream
+  static const size_t pad_env = getenv("GPR_GEMM_PAD") ? (size_t)atoi(getenv("GPR_GEMM_PAD")) : 0;
+  const size_t pad = g.occ1 ? 20 * 1024 : pad_env;
+  gemm_tn_kernel<<<(unsigned)nblk, 256, pad, ctx->ls>>>(a);
   LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -140,11 +140,44 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     ctx->own_stream = true;
   }
   ctx->ls = ctx->stream;
-  if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) {
+  // the lookahead panel stream gets the highest priority: its latency-bound chain
+  // (diag factor + panel TRSM) must win CUs over the big trailing SYRK it overlaps
+  int prio_lo = 0, prio_hi = 0;
+  hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     delete ctx;
     return GPR_E_HIP;
   }
   if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
+  if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
+  // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
+  // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is
+  // on the critical path of the lookahead chain.  GEMM streams get the complement mask.
+  ctx->diag_cus = 0;
+  if (const char* e = getenv("GPR_DIAG_CUS")) ctx->diag_cus = atoi(e);
+  if (ctx->diag_cus > 0) {
+    hipDeviceProp_t prop;
+    hipGetDeviceProperties(&prop, device);
+    const int ncu = prop.multiProcessorCount;
+    uint32_t md[16] = {0}, mr[16] = {0};
+    for (int c = 0; c < ncu && c < 512; ++c) {
+      if (c < ctx->diag_cus) md[c >> 5] |= 1u << (c & 31);
+      else mr[c >> 5] |= 1u << (c & 31);
+    }
+    const uint32_t words = (uint32_t)((ncu + 31) / 32);
+    if (hipExtStreamCreateWithCUMask(&ctx->sdiag, words, md) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&ctx->smain, words, mr) != hipSuccess) {
+      ctx->diag_cus = 0;
+    }
+    const char* pm = getenv("GPR_PANEL_MASK");
+    if (ctx->diag_cus > 0 && (!pm || atoi(pm))) {
+      hipStream_t s2m = nullptr;
+      if (hipExtStreamCreateWithCUMask(&s2m, words, mr) == hipSuccess) {
+        hipStreamDestroy(ctx->stream2);
+        ctx->stream2 = s2m;
+      }
+    }
+  }
   if (hipMalloc((void**)&ctx->dinfo, 64) != hipSuccess) {
     delete ctx;
     return GPR_E_NOMEM;
@@ -160,6 +193,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto e : ctx->sync_events) hipEventDestroy(e);
   if (ctx->stream2) hipStreamDestroy(ctx->stream2);
+  if (ctx->sdiag) hipStreamDestroy(ctx->sdiag);
+  if (ctx->smain) hipStreamDestroy(ctx->smain);
   if (ctx->winv) hipFree(ctx->winv);
   if (ctx->dinfo) hipFree(ctx->dinfo);
   if (ctx->dscratch) hipFree(ctx->dscratch);

@@ -35,31 +35,68 @@ extern "C" void gpr_debug_diag_stamps(unsigned long long* out) {
 
 namespace {
 
-constexpr int DIAG_THREADS = 512;
+constexpr int DIAG_THREADS = 256;
 
-// Factor (mode 1) or only invert an existing factor (mode 0) of one NB x NB diagonal block.
-// mode 1: one launch per panel, block at A + kglob*(lda+1), size kb = min(NB, n-kglob);
-// mode 0: grid = number of blocks, block b at A + b*NB*(lda+1).
-//
-// Register-owned right-looking algorithm: thread (tr, tc) = (t & 31, t >> 5) owns the
-// elements (tr + 32a, tc + 16b) of the block (upper part), so each of the NB sequential
-// steps is: owners of the pivot row publish it to a double-buffered LDS row, ONE barrier,
-// every thread updates its elements from the broadcast row.  The inverse U^{-1} (needed so
-// the panel TRSM becomes an MFMA GEMM) is built the same way (X U = I, right-looking over
-// columns) with U read from an LDS copy.  Padding beyond kb is the identity.
+// ---- blocked diagonal-block kernel ------------------------------------------------------
+// Factor (mode 1) / only invert (mode 0) one NB x NB diagonal block, blocked by SB = 32:
+//   per sub-block K0:  A1 all 4 waves factor the 32x32 diagonal sub-block (thread owns
+//                         4 elements; one barrier per step; pivot via rsq + Newton),
+//                      A2 strip TRSM  U(K0:K0+32, K0+32:) = D^{-T} S(...)  (thread/column),
+//                      A3 trailing update of the rest of the block on FP64 MFMA.
+//   inverse X = U^{-1}: B1 one wave per 32x32 diagonal sub-block inverts it in registers,
+//                       B2 off-diagonal blocks by super-diagonal levels on MFMA,
+//                          X_IJ = -X_II T,  T = sum_{K=I+1..J} U_IK X_KJ  (T never leaves
+//                          the accumulators: the f64 MFMA D layout of register q is exactly
+//                          the B-operand layout of k-step 4q).
+// Everything runs out of LDS/registers: the block is fetched with ONE batch of loads and
+// written back with fire-and-forget stores, because this kernel sits on the critical path
+// of the lookahead chain while the trailing SYRK saturates HBM (a dependent global round
+// trip then costs microseconds).  LDS is kept to ~84 KB (U packed + the diagonal blocks
+// of U^{-1}) so the kernel fits on a CU beside ONE trailing-update GEMM workgroup: with a
+// full-CU footprint it waited ~0.7 ms per call for a CU to drain (measured).  Off-diagonal
+// blocks of U^{-1} go straight to the workspace slot and are re-read by B2 with one batched
+// prefetch per tile.  Padding beyond kb is the identity.
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int pk(int r, int c) { return (c * (c + 1) >> 1) + r; }  // r <= c
+
+// 1/sqrt(x) to ~1 ulp: hardware rsq + one Newton step (shorter dependency chain than the
+// correctly-rounded sqrt + divide; this is the pivot of every sequential step)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x * y;
+  const double r = fma(-h, y, 0.5);
+  return fma(y, r, y);
+}
+
 template <int NB>
-__global__ __launch_bounds__(DIAG_THREADS) void diag_block_kernel(double* __restrict__ A,
+__global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __restrict__ A,
                                                                   size_t lda, int n, int kglob,
                                                                   int* __restrict__ info,
                                                                   double* __restrict__ winv,
                                                                   int mode) {
-  constexpr int LD = NB + 1;
-  constexpr int RA = NB / 32, CB = NB / 16;
-  __shared__ double S[NB * LD];
-  __shared__ double buf[2][NB];
+  constexpr int SB = 32, NSB = NB / SB, NW = DIAG_THREADS / 64;
+  constexpr int PK = NB * (NB + 1) / 2;
+  constexpr int PER = NB * NB / DIAG_THREADS;  // elements per thread in the bulk copies
+  constexpr int PB = SB * (SB + 1) / 2;
+  __shared__ double S[PK];        // U, packed upper (66 KB at NB = 128)
+  __shared__ double Xd[NSB][PB];  // diagonal 32x32 blocks of U^{-1}, packed upper (17 KB)
+  __shared__ double rb[2][NB];
+  __shared__ double wbuf[NW][SB];
+  __shared__ int fail;
   if (*info != 0) return;
-  const int tid = threadIdx.x;
-  const int tr = tid & 31, tc = tid >> 5;
+  // this latency-bound chain shares CUs with the MFMA-saturating trailing update: take
+  // issue priority over the co-resident GEMM waves (FP64 VALU and FP64 MFMA share the
+  // SIMD's FP64 throughput on gfx950)
+  __builtin_amdgcn_s_setprio(3);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   int k0, kb;
   if (mode == 1) {
     k0 = kglob;
@@ -71,144 +108,266 @@ __global__ __launch_bounds__(DIAG_THREADS) void diag_block_kernel(double* __rest
   }
   double* Ab = A + (size_t)k0 + (size_t)k0 * lda;
   STAMP(0);
-  double a[RA][CB];
+  // batched loads (16 in flight per thread per batch, 4 batches at NB = 128), then LDS
+  constexpr int CH = PER < 16 ? PER : 16;
+#pragma unroll 1
+  for (int e0 = 0; e0 < PER; e0 += CH) {
+    double v[CH];
 #pragma unroll
-  for (int ai = 0; ai < RA; ++ai)
-#pragma unroll
-    for (int bi = 0; bi < CB; ++bi) {
-      const int r = tr + 32 * ai, c = tc + 16 * bi;
-      double v = (r == c) ? 1.0 : 0.0;
-      if (r < kb && c < kb && r <= c) v = Ab[(size_t)r + (size_t)c * lda];
-      a[ai][bi] = v;
+    for (int e = 0; e < CH; ++e) {
+      const int idx = tid + (e0 + e) * DIAG_THREADS;
+      const int r = idx % NB, c = idx / NB;
+      v[e] = (r <= c && c < kb) ? Ab[(size_t)r + (size_t)c * lda] : ((r == c) ? 1.0 : 0.0);
     }
-
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int idx = tid + (e0 + e) * DIAG_THREADS;
+      const int r = idx % NB, c = idx / NB;
+      if (r <= c) S[pk(r, c)] = v[e];
+    }
+  }
+  if (tid == 0) fail = 0;
+  __syncthreads();
   STAMP(1);
   if (mode == 1) {
-    for (int j = 0; j < kb; ++j) {
-      const int p = j & 1;
-      if (tr == (j & 31)) {  // owners of row j publish it (entries c < j are never read)
-        const int aj = j >> 5;
+    // A1+A2 ownership in the 32-row band [K0, K0+32) x [K0, NB): thread owns rows
+    // 4 rg + i (i < 4) of columns K0 + cc + 32 cb (cb < NCB).  Row j = 4 jo + jl lives in
+    // slot i = jl (compile-time in the unroll-by-4 inner loop) of the threads rg == jo.
+    constexpr int NCB = NB / SB;
+    const int cc = tid & 31, rg = tid >> 5;
+    for (int sb = 0; sb < NSB; ++sb) {
+      const int K0 = sb * SB;
+      const int W = NB - K0;  // band width
+      // ---- A1+A2: right-looking factorisation of the band (pivots in its first 32 cols)
+      double d[4][NCB];
 #pragma unroll
-        for (int bi = 0; bi < CB; ++bi) {
-          double v = a[0][bi];
+      for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-          for (int ai = 1; ai < RA; ++ai) v = (ai == aj) ? a[ai][bi] : v;
-          buf[p][tc + 16 * bi] = v;
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rg + i, c = cc + 32 * cb;
+          d[i][cb] = (c < W && r <= c) ? S[pk(K0 + r, K0 + c)] : 0.0;
+        }
+      int bad = 0;
+#pragma unroll 1
+      for (int jo = 0; jo < SB / 4; ++jo) {
+#pragma unroll
+        for (int jl = 0; jl < 4; ++jl) {
+          const int j = 4 * jo + jl;
+          double* b = rb[jl & 1];
+          if (rg == jo) {  // owners of band row j publish it
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) b[cc + 32 * cb] = d[jl][cb];
+          }
+          __syncthreads();
+          const double piv = b[j];
+          bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
+          const double ri = rsqrt_nr(piv);
+          const double u = piv * ri;
+          double uc[NCB], ur[4];
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) {
+            const int c = cc + 32 * cb;
+            const double bc = b[c];
+            uc[cb] = (c > j) ? bc * ri : 0.0;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * rg + i;
+            const double br = b[r];
+            ur[i] = (r > j) ? br * ri : 0.0;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+              const double upd = fma(-ur[i], uc[cb], d[i][cb]);
+              if (i == jl) {  // compile-time: this slot holds row j in the owner threads
+                const int c = cc + 32 * cb;
+                const double rowj = (c == j) ? u : ((c > j) ? uc[cb] : d[i][cb]);
+                d[i][cb] = (rg == jo) ? rowj : upd;
+              } else {
+                d[i][cb] = upd;
+              }
+            }
         }
       }
+      if (bad) {
+        if (tid == 0) fail = kglob + K0 + bad;
+      } else {
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * rg + i, c = cc + 32 * cb;
+            if (c < W && r <= c) S[pk(K0 + r, K0 + c)] = d[i][cb];
+          }
+      }
       __syncthreads();
-      const double dj = buf[p][j];
-      if (!(dj > 0.0)) {  // also catches NaN (dpotf2: ajj <= 0 .or. disnan(ajj))
-        if (tid == 0) *info = kglob + j + 1;
+      if (sb == 0) STAMP(5);
+      if (fail) {
+        if (tid == 0) *info = fail;
         return;
       }
-      const double u = sqrt(dj);
-      const double ri = 1.0 / u;
-      double ur[RA], uc[CB];
+      const int R = NB - K0 - SB;  // rows/cols of the block after this sub-block
+      if (R <= 0) break;
+      if (sb == 0) STAMP(6);
+      // ---- A3: U(r, c) -= sum_p U(K0+p, r) U(K0+p, c) for K0+32 <= r <= c < NB, on MFMA
+      {
+        const int nt = R / 16, B0 = K0 + SB;
+        const int ntile = nt * (nt + 1) / 2;
+        for (int t = wv; t < ntile; t += NW) {
+          int tj = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+          while ((tj + 1) * (tj + 2) / 2 <= t) ++tj;
+          while (tj * (tj + 1) / 2 > t) --tj;
+          const int ti = t - tj * (tj + 1) / 2;
+          const int r0 = B0 + 16 * ti, q0 = B0 + 16 * tj;
+          d4v acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int ai = 0; ai < RA; ++ai) {
-        const int r = tr + 32 * ai;
-        const double v = buf[p][r];  // unconditional load, then select (no branch/wait)
-        ur[ai] = (r > j) ? v * ri : 0.0;
-      }
+          for (int kk = 0; kk < SB; kk += 4) {
+            const int p = K0 + kk + (lane >> 4);
+            const double av = S[pk(p, r0 + (lane & 15))];
+            const double bv = S[pk(p, q0 + (lane & 15))];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          }
 #pragma unroll
-      for (int bi = 0; bi < CB; ++bi) {
-        const int c = tc + 16 * bi;
-        const double v = buf[p][c];
-        uc[bi] = (c > j) ? v * ri : 0.0;
-      }
-      // ur/uc are zero outside the trailing block, so the rank-1 update is a no-op there
-      // (elements below the diagonal take garbage that is never stored).  Row/column blocks
-      // that are entirely finished (<= j) are skipped with wave-uniform branches.
-#pragma unroll
-      for (int ai = 0; ai < RA; ++ai) {
-        if (32 * ai + 31 < j) continue;
-        const int r = tr + 32 * ai;
-#pragma unroll
-        for (int bi = 0; bi < CB; ++bi) {
-          if (16 * bi + 15 < j) continue;
-          const int c = tc + 16 * bi;
-          const double upd = fma(-ur[ai], uc[bi], a[ai][bi]);
-          if (32 * ai <= j) {  // this row block contains row j: finalise U[j][c]
-            const double rowj = (c == j) ? u : ((c > j) ? uc[bi] : a[ai][bi]);
-            a[ai][bi] = (r == j) ? rowj : upd;
-          } else {
-            a[ai][bi] = upd;
+          for (int q = 0; q < 4; ++q) {
+            const int r = r0 + (lane >> 4) + 4 * q, c = q0 + (lane & 15);
+            if (r <= c) S[pk(r, c)] -= acc[q];
           }
         }
       }
+      __syncthreads();
+      if (sb == 0) STAMP(7);
     }
   }
-
   STAMP(2);
-  // U (upper) -> LDS copy (and back to global in mode 1)
+  // U (upper) back to global (mode 1): fire-and-forget stores
+  if (mode == 1) {
 #pragma unroll
-  for (int ai = 0; ai < RA; ++ai)
-#pragma unroll
-    for (int bi = 0; bi < CB; ++bi) {
-      const int r = tr + 32 * ai, c = tc + 16 * bi;
-      if (r <= c) {
-        S[r + c * LD] = a[ai][bi];
-        if (mode == 1 && r < kb && c < kb) Ab[(size_t)r + (size_t)c * lda] = a[ai][bi];
-      }
+    for (int e = 0; e < PER; ++e) {
+      const int idx = tid + e * DIAG_THREADS;
+      const int r = idx % NB, c = idx / NB;
+      if (r < kb && c < kb && r <= c) Ab[(size_t)r + (size_t)c * lda] = S[pk(r, c)];
     }
-  // X = U^{-1}: X U = I, right-looking over columns; X owned like U, starts as I.
-#pragma unroll
-  for (int ai = 0; ai < RA; ++ai)
-#pragma unroll
-    for (int bi = 0; bi < CB; ++bi) a[ai][bi] = (tr + 32 * ai == tc + 16 * bi) ? 1.0 : 0.0;
-  __syncthreads();
+  }
   STAMP(3);
-  for (int r = 0; r < kb; ++r) {
-    const int p = r & 1;
-    const double urr = S[r + r * LD];
-    if (tc == (r & 15)) {  // owners of column r finalise it: X[i][r] /= U[r][r]
-      const int br = r >> 4;
+  // ---- B1: wave w inverts diagonal sub-blocks w, w+NW, ... : X D = I, right-looking over
+  // columns r; lane holds X[16h+i][c32]
+  const int c32 = lane & 31, h = lane >> 5;
+  for (int sbi = wv; sbi < NSB; sbi += NW) {
+    const int K0 = sbi * SB;
+    double x[16];
 #pragma unroll
-      for (int ai = 0; ai < RA; ++ai) {
-        double v = a[ai][0];
+    for (int i = 0; i < 16; ++i) x[i] = (16 * h + i == c32) ? 1.0 : 0.0;
+    double* cb = wbuf[wv];
+#pragma unroll 2
+    for (int r = 0; r < SB; ++r) {
+      const double ir = 1.0 / S[pk(K0 + r, K0 + r)];
+      if (c32 == r) {
 #pragma unroll
-        for (int bi = 1; bi < CB; ++bi) v = (bi == br) ? a[ai][bi] : v;
-        const double x = v / urr;
-        const bool fin = (tr + 32 * ai) <= r;
+        for (int i = 0; i < 16; ++i) {
+          x[i] = x[i] * ir;  // rows i > r are zero here
+          cb[16 * h + i] = x[i];
+        }
+      }
+      wave_fence();
+      const double urc = S[pk(K0 + min(r, c32), K0 + c32)];
+      const double uv = (c32 > r) ? urc : 0.0;
 #pragma unroll
-        for (int bi = 0; bi < CB; ++bi) a[ai][bi] = (bi == br && fin) ? x : a[ai][bi];
-        buf[p][tr + 32 * ai] = x;  // entries i > r are never read
+      for (int i = 0; i < 16; ++i) {
+        const int ii = 16 * h + i;
+        const double xv = cb[ii];
+        if (ii <= r) x[i] = fma(-xv, uv, x[i]);
+      }
+      wave_fence();
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ii = 16 * h + i;
+      if (ii <= c32) Xd[sbi][pk(ii, c32)] = x[i];
+      // the diagonal block also goes to the workspace slot (zero below its diagonal)
+      const bool in = (K0 + ii < kb) && (K0 + c32 < kb);
+      winv[(K0 + ii) + (size_t)(K0 + c32) * NB] = (ii <= c32 && in) ? x[i] : 0.0;
+    }
+  }
+  // zero the slot below the diagonal blocks (off-diagonal lower blocks)
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int idx = tid + e * DIAG_THREADS;
+    const int r = idx % NB, c = idx / NB;
+    if ((r >> 5) > (c >> 5)) winv[idx] = 0.0;
+  }
+  __syncthreads();
+  // ---- B2: off-diagonal blocks, level by level; one wave per 16x16 output tile
+  for (int dl = 1; dl < NSB; ++dl) {
+    const int nblk = NSB - dl;
+    for (int t = wv; t < nblk * 4; t += NW) {
+      const int I = t >> 2, ih = t & 1, jh = (t >> 1) & 1, J = I + dl;
+      const int jc = J * SB + 16 * jh + (lane & 15);  // output column (B-operand column)
+      // T[:, jh] for both 16-row halves of the I block: T = sum_K U_IK X_KJ.
+      // X_KJ (K < J) comes from the workspace (previous levels): prefetch it in one batch.
+      d4v T0 = {0.0, 0.0, 0.0, 0.0}, T1 = {0.0, 0.0, 0.0, 0.0};
+      double bpre[(NSB - 2) * (SB / 4) > 0 ? (NSB - 2) * (SB / 4) : 1];
+#pragma unroll
+      for (int Kb2 = 0; Kb2 < NSB - 2; ++Kb2) {
+        const int Kb = I + 1 + Kb2;
+#pragma unroll
+        for (int kq = 0; kq < SB / 4; ++kq) {
+          const int k = Kb * SB + 4 * kq + (lane >> 4);
+          bpre[Kb2 * (SB / 4) + kq] = (Kb < J) ? winv[k + (size_t)jc * NB] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int Kb2 = 0; Kb2 < NSB - 1; ++Kb2) {
+        const int Kb = I + 1 + Kb2;
+        if (Kb > J) break;
+#pragma unroll
+        for (int kq = 0; kq < SB / 4; ++kq) {
+          const int kl = 4 * kq + (lane >> 4), k = Kb * SB + kl;
+          double bv;
+          if (Kb == J) {  // X_JJ from LDS
+            const int jl = jc - J * SB;
+            const double xv = Xd[J][pk(min(kl, jl), jl)];
+            bv = (kl <= jl) ? xv : 0.0;
+          } else {
+            bv = bpre[Kb2 * (SB / 4) + kq];
+          }
+          const double a0 = S[pk(I * SB + (lane & 15), k)];       // U(i, k), i < k
+          const double a1 = S[pk(I * SB + 16 + (lane & 15), k)];
+          T0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv, T0, 0, 0, 0);
+          T1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv, T1, 0, 0, 0);
+        }
+      }
+      // X_IJ[ih rows, jh cols] = - sum_m X_II[i][m] T[m][j]; T register q = k-step 4q
+      d4v acc = {0.0, 0.0, 0.0, 0.0};
+      const int il = 16 * ih + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ml = 4 * q + (lane >> 4);
+        const double xv = Xd[I][pk(min(il, ml), ml)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64((il <= ml) ? xv : 0.0, T0[q], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ml = 16 + 4 * q + (lane >> 4);
+        const double xv = Xd[I][pk(min(il, ml), ml)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64((il <= ml) ? xv : 0.0, T1[q], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = I * SB + 16 * ih + (lane >> 4) + 4 * q;
+        winv[i + (size_t)jc * NB] = (i < kb && jc < kb) ? -acc[q] : 0.0;
       }
     }
-    __syncthreads();
-    double xc[RA], ur[CB];
-#pragma unroll
-    for (int ai = 0; ai < RA; ++ai) {
-      const int i = tr + 32 * ai;
-      const double v = buf[p][i];
-      xc[ai] = (i <= r) ? v : 0.0;
-    }
-#pragma unroll
-    for (int bi = 0; bi < CB; ++bi) {
-      const int jj = tc + 16 * bi;
-      const double v = S[r + jj * LD];
-      ur[bi] = (jj > r) ? v : 0.0;
-    }
-#pragma unroll
-    for (int ai = 0; ai < RA; ++ai) {
-      if (32 * ai > r) continue;            // rows i > r untouched
-#pragma unroll
-      for (int bi = 0; bi < CB; ++bi) {
-        if (16 * bi + 15 <= r) continue;    // columns jj <= r finished
-        a[ai][bi] = fma(-xc[ai], ur[bi], a[ai][bi]);
-      }
-    }
+    __syncthreads();  // workgroup-scope fence: this level's X blocks visible to the next
   }
   STAMP(4);
-  // write U^{-1} (upper, zero below, zero outside kb) to the workspace slot
-#pragma unroll
-  for (int ai = 0; ai < RA; ++ai)
-#pragma unroll
-    for (int bi = 0; bi < CB; ++bi) {
-      const int r = tr + 32 * ai, c = tc + 16 * bi;
-      winv[r + c * NB] = (r <= c && r < kb && c < kb) ? a[ai][bi] : 0.0;
-    }
+#ifdef GPR_DIAG_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    atomicAdd(&g_diag_stamps[8], g_diag_stamps[4] - g_diag_stamps[0]);
+    atomicAdd(&g_diag_stamps[9], 1ull);
+  }
+#endif
 }
 
 // ---- small-RHS triangular solves (TRSV-like, nrhs <= 16 per launch) --------------------
@@ -316,7 +475,20 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   for (int j = k; j < k + kw; j += nb) {
     const int jb = std::min(nb, n - j);
     double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
-    GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
+    if (ctx->diag_cus > 0) {  // hop to the reserved-CU stream and back
+      hipStream_t home = ctx->ls;
+      hipEvent_t e1 = sync_event(ctx, ctx->ev_next++), e2 = sync_event(ctx, ctx->ev_next++);
+      HIP_TRY(ctx, hipEventRecord(e1, home));
+      HIP_TRY(ctx, hipStreamWaitEvent(ctx->sdiag, e1, 0));
+      ctx->ls = ctx->sdiag;
+      const int rc = launch_diag(ctx, A, lda, n, j, wj, 1, 1);
+      ctx->ls = home;
+      if (rc) return rc;
+      HIP_TRY(ctx, hipEventRecord(e2, ctx->sdiag));
+      HIP_TRY(ctx, hipStreamWaitEvent(home, e2, 0));
+    } else {
+      GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
+    }
     if (j + jb >= n) break;
     double* row = A + j + (size_t)(j + jb) * lda;
     GemmArgs g{};
@@ -382,12 +554,15 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
   const int nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
   ctx->fac_valid = false;
   GPR_TRY(ensure_winv(ctx, n, nb));
-  hipStream_t s0 = ctx->stream, s1 = ctx->stream2;
-  HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), s0));
+  hipStream_t user = ctx->stream;
+  hipStream_t s0 = ctx->smain ? ctx->smain : ctx->stream, s1 = ctx->stream2;
+  HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), user));
   size_t ev = 0;
+  ctx->ev_next = 1000;  // events of the diag hops use a separate index range
   hipEvent_t e0 = sync_event(ctx, ev++);
-  HIP_TRY(ctx, hipEventRecord(e0, s0));
+  HIP_TRY(ctx, hipEventRecord(e0, user));
   HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
+  if (s0 != user) HIP_TRY(ctx, hipStreamWaitEvent(s0, e0, 0));
   ctx->ls = s1;
   int rc = factor_panel(ctx, dA, n, lda, 0, std::min(nb2, n));
   hipEvent_t ev_p = sync_event(ctx, ev++);
@@ -414,28 +589,49 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
     ctx->ls = s0;
     if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
     if (rest0 < n) {
-      GemmArgs b{};
-      b.P = dA + k + (size_t)rest0 * lda; b.ldp = lda;
-      b.Q = b.P; b.ldq = lda;
-      b.C = dA + rest0 + (size_t)rest0 * lda; b.ldc = lda;
-      b.M = n - rest0; b.N = n - rest0; b.K = nb2;
-      b.alpha = -1.0; b.beta = 1.0;
-      b.upper = 1;
-      b.info = ctx->dinfo;
-      if ((rc = launch_gemm_tn(ctx, b, TC_SYRK))) break;
+      // b_s as `pieces` launches of ~equal work (column bands [c0, c1) of the upper
+      // trailing matrix), so the lookahead stream gets dispatch opportunities in between
+      const int R = n - rest0;
+      const int pieces = std::max(1, std::min(ctx->syrk_pieces, R / 1024));
+      int c0 = 0;
+      for (int pi = 1; pi <= pieces && !rc; ++pi) {
+        int c1 = pi == pieces ? R : (int)(std::sqrt((double)pi / pieces) * R) / 128 * 128;
+        if (c1 <= c0) continue;
+        GemmArgs b{};
+        b.P = dA + k + (size_t)rest0 * lda; b.ldp = lda;   // rows [0, c1) of the band
+        b.Q = dA + k + (size_t)(rest0 + c0) * lda; b.ldq = lda;
+        b.C = dA + rest0 + (size_t)(rest0 + c0) * lda; b.ldc = lda;
+        b.M = c1; b.N = c1 - c0; b.K = nb2;
+        b.alpha = -1.0; b.beta = 1.0;
+        if (c0 == 0) {
+          b.upper = 1;
+        } else {
+          b.mask_upper = 1;
+          b.mask_off = c0;
+        }
+        b.info = ctx->dinfo;
+        rc = launch_gemm_tn(ctx, b, TC_SYRK);
+        c0 = c1;
+      }
+      if (rc) break;
     }
     ev_b = sync_event(ctx, ev++);
     if (hipEventRecord(ev_b, s0) != hipSuccess) { rc = GPR_E_HIP; break; }
     ev_p = ev_p_next;
   }
-  ctx->ls = s0;
-  hipEvent_t ej = sync_event(ctx, ev++);  // join the panel stream into the main stream
+  ctx->ls = user;
+  hipEvent_t ej = sync_event(ctx, ev++);  // join the panel and main streams into the user's
   HIP_TRY(ctx, hipEventRecord(ej, s1));
-  HIP_TRY(ctx, hipStreamWaitEvent(s0, ej, 0));
+  HIP_TRY(ctx, hipStreamWaitEvent(user, ej, 0));
+  if (s0 != user) {
+    hipEvent_t ek = sync_event(ctx, ev++);
+    HIP_TRY(ctx, hipEventRecord(ek, s0));
+    HIP_TRY(ctx, hipStreamWaitEvent(user, ek, 0));
+  }
   if (rc) return rc;
   int hinfo = 0;
-  HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, s0));
-  HIP_TRY(ctx, hipStreamSynchronize(s0));
+  HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, user));
+  HIP_TRY(ctx, hipStreamSynchronize(user));
   if (info) *info = hinfo;
   if (hinfo == 0) {
     ctx->fac_valid = true;

@@ -50,6 +50,8 @@ int main(int argc, char** argv) {
     {
       unsigned long long st[16];
       gpr_debug_diag_stamps(st);
+      printf("in-kernel diag time: %.2f us avg over %llu calls (all reps)\n", st[8] / 100.0 / (st[9] ? st[9] : 1), st[9]);
+      printf("sb0: A1 %.2f A2 %.2f A3 %.2f us\n", (st[5] - st[1]) / 100.0, (st[6] - st[5]) / 100.0, (st[7] - st[6]) / 100.0);
       printf("last diag stamps (us from start, 100 MHz clock): load %.2f factor %.2f copy %.2f inverse %.2f\n",
              (st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0, (st[4] - st[3]) / 100.0);
     }

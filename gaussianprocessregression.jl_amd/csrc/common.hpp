@@ -41,7 +41,7 @@ struct gpr_ctx {
   bool own_stream = false;
   std::string err;
   int nb = 128;   // inner panel width (diag blocks, in-place panel GEMMs)
-  int nb2 = 768;  // outer panel width = K of the big trailing updates (multiple of nb)
+  int nb2 = 1024;  // outer panel width = K of the big trailing updates (multiple of nb)
   hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
   hipStream_t stream2 = nullptr;  // lookahead panel stream (GEMMs of the panel chain)
   hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
@@ -66,6 +66,8 @@ struct gpr_ctx {
   size_t big_cap = 0;           // doubles
   double* dbig2 = nullptr;
   size_t big2_cap = 0;
+  double* dtrsv = nullptr;      // single-launch triangular sweep hand-off vector (n x 2)
+  size_t trsv_cap = 0;
   double* dxs = nullptr;        // per-part scaled training inputs  (nse x d x n)
   size_t xs_cap = 0;
   double* dxps = nullptr;       // per-part scaled second inputs    (nse x d x m)

@@ -26,7 +26,15 @@
 
 namespace {
 
-constexpr int TM = 128, TN = 128, TK = 16, LDT = TK + 1;
+constexpr int TM = 128, TN = 128, TK = 16, LDT = TK;
+// LDS rows hold the 16 k-values of one column as eight 16-B chunks; chunk c of row r is
+// stored at chunk position c ^ ((r >> 1) & 7).  Lane l of an MFMA fragment reads row l & 15,
+// chunk (l >> 4) + 4p with ONE ds_read_b128 (k-steps 2p and 2p+1): with this swizzle each of
+// the four 16-lane groups of ds_read_b128 hits 16 distinct bank quads (conflict-free), and
+// the 8-lane groups of the 16-B stores write one whole row each.
+__device__ __forceinline__ int lds_idx(int row, int chunk) {
+  return row * LDT + ((chunk ^ ((row >> 1) & 7)) << 1);
+}
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 struct GemmK {
@@ -35,15 +43,11 @@ struct GemmK {
   int gm, gn;           // super-tile edges (tiles)
   int xcd_remap;
   int super_m;          // super-tiles along m (general grid)
+  int dbg;              // diagnostics: every tile loads the first panels (L2-resident)
 };
 
-__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
+__device__ __forceinline__ bool tile_coords(const GemmK& a, int& m0, int& n0) {
   const GemmArgs& g = a.g;
-  if (g.info && *g.info != 0) return;
-  __shared__ double Ps[2][TM * LDT];
-  __shared__ double Qs[2][TN * LDT];
-  __shared__ double red[2][TN];
-
   // XCD-aware, super-tile-grouped tile order.  Blocks b and b+8 share an XCD (round-robin
   // dispatch), so the bijective remap hands each XCD a contiguous range of logical ids;
   // logical ids walk GxG super-tiles, so the P/Q panels of the ~64 tiles an XCD has in
@@ -67,77 +71,17 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
     SJ = sidx / a.super_m;
   }
   const int tm = SI * Gm + (wl % Gm), tn = SJ * Gn + (wl / Gm);
-  if (tm >= a.tiles_m || tn >= a.tiles_n || (g.upper && tm > tn)) return;
-  const int m0 = tm * TM, n0 = tn * TN;
-  if (g.mask_upper && m0 > n0 + TN - 1 + g.mask_off) return;  // tile entirely below diagonal
+  if (tm >= a.tiles_m || tn >= a.tiles_n || (g.upper && tm > tn)) return false;
+  m0 = tm * TM;
+  n0 = tn * TN;
+  return !(g.mask_upper && m0 > n0 + TN - 1 + g.mask_off);  // tile entirely below diagonal
+}
+
+// C = alpha * acc (o E) + beta * C on the tile, optional column sum-of-squares into norm_out.
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, d4 (&acc)[4][4], int m0, int n0,
+                                              double* red) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
-
-  const int kbeg = g.kfrom_n ? n0 : 0;
-  const int kend = g.K;
-  const int nst = kend > kbeg ? (kend - kbeg + TK - 1) / TK : 0;
-
-  d4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-
-  double rp[8], rq[8];
-  // global -> registers for stage s
-  auto gload = [&](int s) {
-    const int k0 = kbeg + s * TK;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int idx = tid + 256 * r;
-      const int col = idx >> 4, kk = idx & 15;
-      const int k = k0 + kk;
-      const bool kin = k < kend;
-      const int m = m0 + col, n = n0 + col;
-      rp[r] = (kin && m < g.M) ? g.P[(size_t)k + (size_t)m * g.ldp] : 0.0;
-      double q = (kin && n < g.N) ? g.Q[(size_t)k + (size_t)n * g.ldq] : 0.0;
-      if (g.qscale) q *= (kin ? g.qscale[k] : 0.0);
-      rq[r] = q;
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int idx = tid + 256 * r;
-      const int col = idx >> 4, kk = idx & 15;
-      Ps[buf][col * LDT + kk] = rp[r];
-      Qs[buf][col * LDT + kk] = rq[r];
-    }
-  };
-
-  if (nst > 0) {
-    gload(0);
-    lstore(0);
-    __syncthreads();
-  }
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nst) gload(s + 1);
-    const double* ps = Ps[buf];
-    const double* qs = Qs[buf];
-#pragma unroll
-    for (int k4 = 0; k4 < TK / 4; ++k4) {
-      double af[4], bf[4];
-      const int kk = k4 * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = qs[(wn * 64 + i * 16 + (lane & 15)) * LDT + kk];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = ps[(wm * 64 + j * 16 + (lane & 15)) * LDT + kk];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
-    if (s + 1 < nst) lstore(buf ^ 1);
-    __syncthreads();
-  }
-
   // ---- epilogue: all loads first (C, E), then all stores -- interleaving them through
   // possibly-aliasing pointers would serialise one HBM round trip per element.
   double* __restrict__ Cp = g.C;
@@ -181,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
         nsum += __shfl_xor(nsum, 2);
         nsum += __shfl_xor(nsum, 4);
         nsum += __shfl_xor(nsum, 8);
-        if ((lane & 15) == 0) red[wm][wn * 64 + i * 16 + (lane >> 4) + 4 * r] = nsum;
+        if ((lane & 15) == 0) red[wm * TN + wn * 64 + i * 16 + (lane >> 4) + 4 * r] = nsum;
       }
     }
   }
@@ -189,12 +133,318 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
     __syncthreads();
     if (tid < TN) {
       const int n = n0 + tid;
-      if (n < g.N) g.norm_out[n] -= red[0][tid] + red[1][tid];
+      if (n < g.N) g.norm_out[n] -= red[tid] + red[TN + tid];
     }
   }
 }
 
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
+  const GemmArgs& g = a.g;
+  if (g.info && *g.info != 0) return;
+  __shared__ double Ps[2][TM * LDT];
+  __shared__ double Qs[2][TN * LDT];
+  __shared__ double red[2][TN];
+
+  int m0, n0;
+  if (!tile_coords(a, m0, n0)) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+
+  const int kbeg = g.kfrom_n ? n0 : 0;
+  const int kend = g.K;
+  const int nst = kend > kbeg ? (kend - kbeg + TK - 1) / TK : 0;
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // VEC: 16-B loads of k-pairs (8 lanes cover one 128-B column segment), branch-free with
+  // clamped addresses; out-of-range elements are zeroed when the stage is written to LDS.
+  // Needs 16-B aligned operands, even ld and even K (checked by the launcher), no qscale.
+  // Scalar path: one f64 per lane per load, any alignment, optional qscale.
+  constexpr int NR = VEC ? 4 : 8;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  d2 vp[VEC ? 4 : 1], vq[VEC ? 4 : 1];
+  double rp[VEC ? 1 : 8], rq[VEC ? 1 : 8];
+  // global -> registers for stage s
+  auto gload = [&](int s) {
+    const int k0 = kbeg + s * TK;
+    if constexpr (VEC) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int idx = tid + 256 * r;
+        const int col = idx >> 3, k = k0 + 2 * (idx & 7);
+        const int kc = k < kend ? k : kbeg;
+        const int m = min((a.dbg ? 0 : m0) + col, g.M - 1), n = min((a.dbg ? 0 : n0) + col, g.N - 1);
+        vp[r] = *reinterpret_cast<const d2*>(g.P + (size_t)kc + (size_t)m * g.ldp);
+        vq[r] = *reinterpret_cast<const d2*>(g.Q + (size_t)kc + (size_t)n * g.ldq);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int idx = tid + 256 * r;
+        const int col = idx >> 4, kk = idx & 15;
+        const int k = k0 + kk;
+        const bool kin = k < kend;
+        const int m = m0 + col, n = n0 + col;
+        rp[r] = (kin && m < g.M) ? g.P[(size_t)k + (size_t)m * g.ldp] : 0.0;
+        double q = (kin && n < g.N) ? g.Q[(size_t)k + (size_t)n * g.ldq] : 0.0;
+        if (g.qscale) q *= (kin ? g.qscale[k] : 0.0);
+        rq[r] = q;
+      }
+    }
+  };
+  auto lstore = [&](int buf, int s) {
+    const int k0 = kbeg + s * TK;
+    if constexpr (VEC) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int idx = tid + 256 * r;
+        const int col = idx >> 3, kp = idx & 7;
+        const bool kin = k0 + 2 * kp < kend;
+        const d2 z = {0.0, 0.0};
+        *reinterpret_cast<d2*>(&Ps[buf][lds_idx(col, kp)]) = (kin && m0 + col < g.M) ? vp[r] : z;
+        *reinterpret_cast<d2*>(&Qs[buf][lds_idx(col, kp)]) = (kin && n0 + col < g.N) ? vq[r] : z;
+      }
+    } else {
+      (void)k0;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int idx = tid + 256 * r;
+        const int col = idx >> 4, kk = idx & 15;
+        Ps[buf][lds_idx(col, kk >> 1) + (kk & 1)] = rp[r];
+        Qs[buf][lds_idx(col, kk >> 1) + (kk & 1)] = rq[r];
+      }
+    }
+  };
+
+  if (nst > 0) {
+    gload(0);
+    lstore(0, 0);
+    __syncthreads();
+  }
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) gload(s + 1);
+    const double* ps = Ps[buf];
+    const double* qs = Qs[buf];
+    // k-step 2p+h, lane group g = lane >> 4 consumes k = 2 (g + 4p) + h for both operands
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int ch = (lane >> 4) + 4 * p;
+      d2 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const d2*>(&qs[lds_idx(wn * 64 + i * 16 + (lane & 15), ch)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[j] = *reinterpret_cast<const d2*>(&ps[lds_idx(wm * 64 + j * 16 + (lane & 15), ch)]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i][h], bf[j][h], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nst) lstore(buf ^ 1, s + 1);
+    __syncthreads();
+  }
+
+  gemm_epilogue(g, acc, m0, n0, &red[0][0]);
+}
+
+// ---- deep-pipelined variant: one workgroup per CU, four LDS stages fed by LDS-DMA ------
+// One wave per SIMD keeps the f64 matrix pipe full on its own (back-to-back
+// v_mfma_f64_16x16x4 from one wave: 77.7 TF/s measured, tools/probe/mfma_f64_peak.hip), so
+// this variant spends the doubled register budget (launch bounds 256 x 1) on a second
+// fragment set instead of a second workgroup: while stage s's 64 MFMAs per wave issue, the
+// ds_read_b128 of stage s+1 are already in flight, and the global->LDS DMA
+// (global_load_lds_dwordx4, no VGPRs, swizzle applied on the source address) runs 2-3
+// stages ahead.  Per stage: one counted vmcnt wait (own DMA of stage s+1 retired) and ONE
+// raw s_barrier (stage s+1 visible to all waves; stage s-1's buffer free for the DMA of
+// stage s+3).  Eligible when K - kbeg is a multiple of 16, operands 16-B aligned with even
+// leading dimensions and no qscale (the launcher checks; other calls use gemm_tn_kernel).
+// acc = 0, produced in AGPRs (an MFMA with zero operands and inline-constant C = 0), so every
+// definition of the accumulators is AGPR-class and the loop never copies them
+__device__ __forceinline__ void mfma_agpr_zero(d4& acc) {
+  asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %1, 0" : "=a"(acc) : "v"(0.0));
+}
+
+template <int VM>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+}
+
+constexpr int PBUF = 4;  // LDS stages of the pipelined kernels
+
+// Stage image: TKS doubles per row (NCH = TKS/2 chunks of 16 B), chunk c of row r stored at
+// c ^ swz(r): conflict-free for the 16-lane groups of ds_read_b128 (checked exhaustively for
+// both row lengths: NCH = 8 -> (r >> 1) & 7, NCH = 4 -> (r >> 1) & 2).
+template <int TKS>
+__device__ __forceinline__ int pipe_swz(int row) {
+  return TKS == 16 ? ((row >> 1) & 7) : ((row >> 1) & 2);
+}
+template <int TKS>
+__device__ __forceinline__ int pipe_idx(int row, int chunk) {
+  return row * TKS + ((chunk ^ pipe_swz<TKS>(row)) << 1);
+}
+
+// TKS = 16, OCC = 1: one workgroup per CU (512 registers per lane), 32-KB stages, 64 MFMAs
+//   per wave per stage -- best for long K (72 TF/s at 8192^3 vs 65 for gemm_tn_kernel).
+// TKS = 8, OCC = 2: two workgroups per CU, 16-KB stages, 32 MFMAs per stage -- a second
+//   workgroup hides each tile's prologue fill and C epilogue, which matter at short K (the
+//   K = nb2 trailing updates of POTRF and the TRSM).
+template <int TKS>
+__device__ __forceinline__ void gemm_tn_pipe_body(const GemmK& a) {
+  constexpr int STAGE_D = (TM + TN) * TKS;      // doubles per stage (P image, then Q)
+  constexpr int NCH = TKS / 2;                  // 16-B chunks per row
+  constexpr int ROWS_PER_DMA = 64 / NCH;        // rows covered by one wave-wide 1-KB DMA
+  constexpr int NDMA = TM / (4 * ROWS_PER_DMA); // DMA instructions per wave per operand
+  constexpr int VM_STAGE = 2 * NDMA;            // vmcnt increments per stage
+  constexpr int NP = TKS / 8;                   // fragment blocks (2 k-steps each) per stage
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const GemmArgs& g = a.g;
+  if (g.info && *g.info != 0) return;
+  __shared__ double lds[PBUF * STAGE_D + 2 * TN];
+  int m0, n0;
+  if (!tile_coords(a, m0, n0)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  const int kbeg = g.kfrom_n ? n0 : 0;
+  const int nst = (g.K - kbeg) / TKS;
+
+  // DMA sources: instruction r of wave w fills rows ROWS_PER_DMA (4r + w) + (L / NCH); lane
+  // L lands at physical chunk L % NCH of its row, so it fetches the logical chunk
+  // (L % NCH) ^ swz(row) (the swizzle is applied on the source side; LDS-DMA writes
+  // lane-linearly).  Rows past M/N are clamped: a row of P only feeds its own output row,
+  // which is never stored.
+  const double* srcP[NDMA];
+  const double* srcQ[NDMA];
+#pragma unroll
+  for (int r = 0; r < NDMA; ++r) {
+    const int row = ROWS_PER_DMA * (4 * r + w) + lane / NCH;
+    const int c = (lane % NCH) ^ pipe_swz<TKS>(row);
+    srcP[r] = g.P + kbeg + 2 * c + (size_t)min(m0 + row, g.M - 1) * g.ldp;
+    srcQ[r] = g.Q + kbeg + 2 * c + (size_t)min(n0 + row, g.N - 1) * g.ldq;
+  }
+  // DMA of stage s into buffer s % PBUF.  Stages past the end re-fetch the last stage into a
+  // buffer that is never read again: the loop body stays branch-free (one register
+  // assignment for the accumulators) and the vmcnt count uniform.
+  auto issue = [&](int s) {
+    double* base = lds + (s % PBUF) * STAGE_D;
+    const size_t ko = (size_t)min(s, nst - 1) * TKS;
+#pragma unroll
+    for (int r = 0; r < NDMA; ++r) {
+      __builtin_amdgcn_global_load_lds(srcP[r] + ko, base + (4 * r + w) * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(srcQ[r] + ko, base + TM * TKS + (4 * r + w) * 128, 16, 0, 0);
+    }
+  };
+  // fragment set of one stage: [p][i] Q-side (A operand), [p][4 + j] P-side (B operand);
+  // lane group g = lane >> 4 reads chunk g + 4p, i.e. k = 2 (g + 4p) + h for k-step 2p + h
+  auto read_frags = [&](d2 (&F)[NP][8], int s) {
+    const double* ps = lds + (s % PBUF) * STAGE_D;
+    const double* qs = ps + TM * TKS;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int ch = (lane >> 4) + 4 * p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        F[p][i] = *reinterpret_cast<const d2*>(&qs[pipe_idx<TKS>(wn * 64 + i * 16 + (lane & 15), ch)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        F[p][4 + j] = *reinterpret_cast<const d2*>(&ps[pipe_idx<TKS>(wm * 64 + j * 16 + (lane & 15), ch)]);
+    }
+  };
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mfma_agpr_zero(acc[i][j]);
+  auto mfma_stage = [&](const d2 (&F)[NP][8]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[p][i][h], F[p][4 + j][h], acc[i][j], 0, 0, 0);
+  };
+  // one pipeline step: stage s computes from Fc while stage s+1's fragments load into Fn
+  // (past the end they read a stale buffer and are discarded)
+  auto step = [&](int s, d2 (&Fc)[NP][8], d2 (&Fn)[NP][8]) {
+    wait_vmcnt<VM_STAGE>();  // own DMA of stage s+1 retired, stage s+2 still in flight
+    __builtin_amdgcn_s_barrier();
+    issue(s + 3);
+    read_frags(Fn, s + 1);
+    mfma_stage(Fc);
+    // interleave: the DMAs one per MFMA, then the fragment reads one per two MFMAs, so the
+    // matrix pipe never waits behind a block of memory instructions
+#pragma unroll
+    for (int t = 0; t < VM_STAGE; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    }
+#pragma unroll
+    for (int t = 0; t < 8 * NP; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 32 * NP - VM_STAGE - 16 * NP, 0);
+    // retire Fn's reads here (they completed under the MFMAs): lgkmcnt holds at most 15, so
+    // the compiler would otherwise wait for ALL next-stage reads before the first MFMA of
+    // the next step.  A real s_waitcnt (builtin), which the waitcnt pass accounts for.
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+  };
+
+  d2 F0[NP][8], F1[NP][8];
+  if (nst > 0) {
+    issue(0);
+    issue(1);
+    issue(2);
+    wait_vmcnt<2 * VM_STAGE>();
+    __builtin_amdgcn_s_barrier();
+    read_frags(F0, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  int s = 0;
+  for (; s + 1 < nst; s += 2) {
+    step(s, F0, F1);
+    step(s + 1, F1, F0);
+  }
+  if (s < nst) mfma_stage(F0);
+  wait_vmcnt<0>();
+  __syncthreads();  // the epilogue's norm reduction reuses LDS
+  gemm_epilogue(g, acc, m0, n0, lds + PBUF * STAGE_D);
+}
+
+__global__ __launch_bounds__(256, 1) void gemm_tn_pipe16_kernel(GemmK a) { gemm_tn_pipe_body<16>(a); }
+__global__ __launch_bounds__(256, 2) void gemm_tn_pipe8_kernel(GemmK a) { gemm_tn_pipe_body<8>(a); }
+
 }  // namespace
+
+// GPR_GEMM_PIPE: 1 = the 1-WG/CU variant, 2 (default) = the 2-WG/CU variant (faster at every
+// measured shape: 74.3 vs 71.9 TF/s at 8192^3, 66.3 vs 52.0 at 16384^2 x 768), 3 = by K
+static int pipe_env() {
+  static const int m = getenv("GPR_GEMM_PIPE") ? atoi(getenv("GPR_GEMM_PIPE")) : 2;
+  return m;
+}
+
+static bool pipe_off() {
+  static const bool off = getenv("GPR_GEMM_NOPIPE") != nullptr;
+  return off;
+}
+
+static bool vec_off() {
+  static const bool off = getenv("GPR_GEMM_SCALAR") != nullptr;
+  return off;
+}
 
 int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   if (g.M <= 0 || g.N <= 0) return 0;
@@ -206,6 +456,8 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   static const int genv = getenv("GPR_GEMM_GROUP") ? atoi(getenv("GPR_GEMM_GROUP")) : 8;
   static const int xenv = getenv("GPR_GEMM_XCD") ? atoi(getenv("GPR_GEMM_XCD")) : 1;
   a.xcd_remap = xenv;
+  static const int dbg = getenv("GPR_GEMM_DBG_L2") ? 1 : 0;
+  a.dbg = dbg;
   a.gm = std::max(1, std::min(genv, a.tiles_m));
   a.gn = std::max(1, std::min(genv, a.tiles_n));
   if (g.upper) a.gn = a.gm;
@@ -232,7 +484,22 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   // every CU to a concurrent (lookahead) stream
   static const size_t pad_env = getenv("GPR_GEMM_PAD") ? (size_t)atoi(getenv("GPR_GEMM_PAD")) : 0;
   const size_t pad = g.occ1 ? 20 * 1024 : pad_env;
-  gemm_tn_kernel<<<(unsigned)nblk, 256, pad, ctx->ls>>>(a);
+  const bool vec = !g.qscale && ((uintptr_t)g.P & 15) == 0 && ((uintptr_t)g.Q & 15) == 0 &&
+                   (g.ldp & 1) == 0 && (g.ldq & 1) == 0 && (g.K & 1) == 0 &&
+                   !vec_off();
+  // pipelined variants need K - kbeg to be a whole number of stages (kbeg is 0 or a
+  // multiple of TN); long K goes to the one-workgroup-per-CU variant
+  const int pipe_mode = pipe_off() ? 0 : pipe_env();
+  const bool pipe = vec && (g.K % TK) == 0 && !g.occ1 && pipe_mode != 0;
+  const bool long_k = pipe_mode == 1 || (pipe_mode == 3 && g.K >= 2048);
+  if (pipe && long_k)
+    gemm_tn_pipe16_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
+  else if (pipe)
+    gemm_tn_pipe8_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
+  else if (vec)
+    gemm_tn_kernel<true><<<(unsigned)nblk, 256, pad, ctx->ls>>>(a);
+  else
+    gemm_tn_kernel<false><<<(unsigned)nblk, 256, pad, ctx->ls>>>(a);
   LAUNCH_CHECK(ctx);
   return 0;
 }

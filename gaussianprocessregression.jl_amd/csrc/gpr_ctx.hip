@@ -200,6 +200,7 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dscratch) hipFree(ctx->dscratch);
   if (ctx->dbig) hipFree(ctx->dbig);
   if (ctx->dbig2) hipFree(ctx->dbig2);
+  if (ctx->dtrsv) hipFree(ctx->dtrsv);
   if (ctx->dxs) hipFree(ctx->dxs);
   if (ctx->dxps) hipFree(ctx->dxps);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);

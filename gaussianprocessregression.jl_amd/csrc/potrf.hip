@@ -444,6 +444,237 @@ __global__ __launch_bounds__(256) void gemv_n_update_kernel(const double* __rest
     if (c < nrhs) y[(size_t)r + (size_t)c * ldy] -= acc[c];
 }
 
+// ---- single-launch blocked triangular sweeps (dpotrs, 1-2 right-hand sides per launch, nb = 128) ------------
+// One workgroup per 128-row block, handed out by an atomic ticket so that every block a
+// workgroup depends on belongs to a workgroup that is already running. Block results are
+// published in order (a block can only finish after all blocks before it in the sweep), so
+// one monotonic "blocks done" counter replaces per-block flags. Producer: plain stores ->
+// vmcnt drain -> barrier -> agent release -> relaxed counter store; consumer: relaxed poll
+// by lane 0 of each wave -> agent acquire -> loads (MI355X guide, inter-workgroup hand-off).
+// The hand-off vector lives in its own buffer (hand) that is never read before it is
+// written inside the launch, so no L2 line of it can be stale on another XCD.
+// sync[0] = ticket, sync[1] = blocks done; both zeroed before the launch.
+constexpr int SW_NB = 128, SW_THREADS = 512, SW_COLS = SW_NB / (SW_THREADS / 64);
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Block until at least `need` blocks are published; `known` caches the last observed count.
+__device__ __forceinline__ void sweep_wait(int* sync, int need, int& known, int lane) {
+  if (known >= need) return;
+  int v = 0;
+  if (lane == 0) {
+    while ((v = __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need)
+      __builtin_amdgcn_s_sleep(1);
+  }
+  known = __shfl(v, 0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void sweep_publish(int* sync, int value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&sync[1], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Forward sweep U^T z = b: block b needs sum_{k<b} U[k-rows, b-cols]^T z_k, a column-dot per
+// b-column; each lane keeps partial dots over rows (2l, 2l+1) for its wave's 16 columns and
+// reduces across the wave once at the end. Then z_b = W_b^T r_b (W_b = U_bb^{-1}).
+template <int NR>
+__global__ __launch_bounds__(SW_THREADS) void trsv_fwd_sweep_kernel(
+    const double* __restrict__ U, size_t ldu, int n, const double* __restrict__ W,
+    double* __restrict__ B, size_t ldb, double* hand, int* sync) {
+  __shared__ int sblk;
+  __shared__ double rs[SW_NB * NR];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) sblk = atomicAdd(&sync[0], 1);
+  __syncthreads();
+  const int b = sblk;
+  const int c0 = b * SW_NB, kb = min(SW_NB, n - c0);
+  const int i0 = 2 * lane;
+  const double* Wb = W + (size_t)b * SW_NB * SW_NB;
+  double w0[SW_COLS], w1[SW_COLS];
+#pragma unroll
+  for (int jj = 0; jj < SW_COLS; ++jj) {
+    const int j = w * SW_COLS + jj;
+    const double* col = Wb + (size_t)j * SW_NB;
+    w0[jj] = (j < kb && i0 <= j) ? col[i0] : 0.0;
+    w1[jj] = (j < kb && i0 + 1 <= j) ? col[i0 + 1] : 0.0;
+  }
+  double p[SW_COLS][NR];
+#pragma unroll
+  for (int jj = 0; jj < SW_COLS; ++jj)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) p[jj][r] = 0.0;
+  int known = 0;
+  for (int k = 0; k < b; ++k) {
+    const double* tile = U + (size_t)k * SW_NB + i0 + (size_t)(c0 + w * SW_COLS) * ldu;
+    double u0[SW_COLS], u1[SW_COLS];
+#pragma unroll
+    for (int jj = 0; jj < SW_COLS; ++jj) {
+      const bool ok = w * SW_COLS + jj < kb;
+      u0[jj] = ok ? tile[(size_t)jj * ldu] : 0.0;
+      u1[jj] = ok ? tile[(size_t)jj * ldu + 1] : 0.0;
+    }
+    sweep_wait(sync, k + 1, known, lane);
+    double z0[NR], z1[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      z0[r] = hand[(size_t)r * n + k * SW_NB + i0];
+      z1[r] = hand[(size_t)r * n + k * SW_NB + i0 + 1];
+    }
+#pragma unroll
+    for (int jj = 0; jj < SW_COLS; ++jj)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) p[jj][r] = fma(u0[jj], z0[r], fma(u1[jj], z1[r], p[jj][r]));
+  }
+  // r_b = b_b - partial sums
+#pragma unroll
+  for (int jj = 0; jj < SW_COLS; ++jj) {
+    const int j = w * SW_COLS + jj;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const double s = wave_sum(p[jj][r]);
+      if (lane == 0) rs[j * NR + r] = j < kb ? B[(size_t)(c0 + j) + (size_t)r * ldb] - s : 0.0;
+    }
+  }
+  __syncthreads();
+  // z_m = sum_{i <= m} W[i][m] r_i
+#pragma unroll
+  for (int jj = 0; jj < SW_COLS; ++jj) {
+    const int m = w * SW_COLS + jj;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const double s = wave_sum(fma(w0[jj], rs[i0 * NR + r], w1[jj] * rs[(i0 + 1) * NR + r]));
+      if (lane == 0 && m < kb) {
+        hand[(size_t)r * n + c0 + m] = s;
+        B[(size_t)(c0 + m) + (size_t)r * ldb] = s;
+      }
+    }
+  }
+  sweep_publish(sync, b + 1);
+}
+
+// Backward sweep U x = z: block b (rows) needs sum_{k>b} U[b-rows, k-cols] x_k, a column
+// AXPY: lane keeps rows (2l, 2l+1), wave w columns 16w.., reduced across waves in LDS.
+template <int NR>
+__global__ __launch_bounds__(SW_THREADS) void trsv_bwd_sweep_kernel(
+    const double* __restrict__ U, size_t ldu, int n, const double* __restrict__ W,
+    double* __restrict__ B, size_t ldb, double* hand, int* sync) {
+  constexpr int NW = SW_THREADS / 64;
+  __shared__ int sblk;
+  __shared__ double part[NW][SW_NB * NR];
+  __shared__ double rs[SW_NB * NR];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nblk = (n + SW_NB - 1) / SW_NB;
+  if (tid == 0) sblk = atomicAdd(&sync[0], 1);
+  __syncthreads();
+  const int t = sblk;
+  const int b = nblk - 1 - t;
+  const int r0 = b * SW_NB, kb = min(SW_NB, n - r0);
+  const int i0 = 2 * lane;
+  const bool ok0 = i0 < kb, ok1 = i0 + 1 < kb;
+  const double* Wb = W + (size_t)b * SW_NB * SW_NB;
+  double w0[SW_COLS], w1[SW_COLS];
+#pragma unroll
+  for (int jj = 0; jj < SW_COLS; ++jj) {
+    const int i = w * SW_COLS + jj;  // W column
+    const double* col = Wb + (size_t)i * SW_NB;
+    w0[jj] = (i < kb && i0 <= i) ? col[i0] : 0.0;
+    w1[jj] = (i < kb && i0 + 1 <= i) ? col[i0 + 1] : 0.0;
+  }
+  double a0[NR], a1[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) a0[r] = a1[r] = 0.0;
+  int known = 0;
+  for (int k = nblk - 1; k > b; --k) {
+    const int kk = min(SW_NB, n - k * SW_NB);
+    const double* tile = U + (size_t)r0 + i0 + (size_t)(k * SW_NB + w * SW_COLS) * ldu;
+    double u0[SW_COLS], u1[SW_COLS];
+#pragma unroll
+    for (int jj = 0; jj < SW_COLS; ++jj) {
+      const bool ok = w * SW_COLS + jj < kk;
+      u0[jj] = ok ? tile[(size_t)jj * ldu] : 0.0;
+      u1[jj] = ok ? tile[(size_t)jj * ldu + 1] : 0.0;
+    }
+    sweep_wait(sync, nblk - k, known, lane);
+#pragma unroll
+    for (int jj = 0; jj < SW_COLS; ++jj) {
+      const int j = w * SW_COLS + jj;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const double x = j < kk ? hand[(size_t)r * n + k * SW_NB + j] : 0.0;
+        a0[r] = fma(u0[jj], x, a0[r]);
+        a1[r] = fma(u1[jj], x, a1[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    part[w][i0 * NR + r] = a0[r];
+    part[w][(i0 + 1) * NR + r] = a1[r];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < SW_NB * NR; idx += SW_THREADS) {
+    const int i = idx / NR, r = idx - i * NR;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += part[q][idx];
+    rs[idx] = i < kb ? B[(size_t)(r0 + i) + (size_t)r * ldb] - s : 0.0;
+  }
+  __syncthreads();
+  // x_m = sum_{i >= m} W[m][i] r_i
+#pragma unroll
+  for (int r = 0; r < NR; ++r) a0[r] = a1[r] = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < SW_COLS; ++jj) {
+    const int i = w * SW_COLS + jj;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const double x = rs[i * NR + r];
+      a0[r] = fma(w0[jj], x, a0[r]);
+      a1[r] = fma(w1[jj], x, a1[r]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    part[w][i0 * NR + r] = a0[r];
+    part[w][(i0 + 1) * NR + r] = a1[r];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < SW_NB * NR; idx += SW_THREADS) {
+    const int i = idx / NR, r = idx - i * NR;
+    if (i >= kb) continue;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += part[q][idx];
+    hand[(size_t)r * n + r0 + i] = s;
+    B[(size_t)(r0 + i) + (size_t)r * ldb] = s;
+  }
+  (void)ok0;
+  (void)ok1;
+  sweep_publish(sync, t + 1);
+}
+
+template <int NR>
+static void launch_sweeps(gpr_ctx* ctx, const double* U, size_t ldu, int n, double* B,
+                          size_t ldb, int* sync) {
+  const int nblk = (n + SW_NB - 1) / SW_NB;
+  trsv_fwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
+                                                                  ctx->dtrsv, sync);
+  trsv_bwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
+                                                                  ctx->dtrsv, sync + 2);
+}
+
 int launch_diag(gpr_ctx* ctx, double* A, int lda, int n, int kglob, double* winv, int mode,
                 int nblocks) {
   const int nb = ctx->nb;
@@ -723,6 +954,22 @@ int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   const int nb = ctx->nb;
   const int nblk = (n + nb - 1) / nb;
+  if (nb == SW_NB && !getenv("GPR_POTRS_LEGACY")) {
+    GPR_TRY(ensure_buf(ctx, &ctx->dtrsv, &ctx->trsv_cap, (size_t)n * 2));
+    int* sync = ctx->dinfo + 4;  // dinfo[4..7]: fwd ticket/done, bwd ticket/done
+    for (int c0 = 0; c0 < nrhs; c0 += 2) {
+      const int nc = std::min(2, nrhs - c0);
+      double* B = dB + (size_t)c0 * ldb;
+      HIP_TRY(ctx, hipMemsetAsync(sync, 0, 4 * sizeof(int), ctx->stream));
+      TimerScope ts(ctx, TC_OTHER, 0.0);
+      if (nc == 1)
+        launch_sweeps<1>(ctx, dU, ldu, n, B, ldb, sync);
+      else
+        launch_sweeps<2>(ctx, dU, ldu, n, B, ldb, sync);
+      LAUNCH_CHECK(ctx);
+    }
+    return 0;
+  }
   for (int c0 = 0; c0 < nrhs; c0 += RHS_CHUNK) {
     const int nc = std::min(RHS_CHUNK, nrhs - c0);
     double* B = dB + (size_t)c0 * ldb;

@@ -190,7 +190,8 @@ def test_posdef_exception_from_model():
 # ---------------------------------------------------------------------------------------
 # a6/a7 solves, K^{-1}
 # ---------------------------------------------------------------------------------------
-@pytest.mark.parametrize("n,nrhs", [(300, 1), (257, 3), (129, 20)])
+@pytest.mark.parametrize("n,nrhs", [(300, 1), (257, 3), (129, 20), (1, 1), (128, 2), (1000, 1),
+                                    (3001, 5), (4096, 2)])
 def test_potrs(n, nrhs):
     ctx = G.Context(0)
     A = _spd(n, seed=7)
@@ -203,6 +204,26 @@ def test_potrs(n, nrhs):
     X = ctx.host(dB)
     Xo = O.cho_solve_upper(sla.cholesky(A, lower=False), B)
     assert relnorm(X, Xo) < 1e-11
+
+
+def test_potrs_repeated_sweeps_identical():
+    """The single-launch sweeps hand blocks between workgroups through flags: repeated calls
+    must give bit-identical results (any stale hand-off would show up as a difference)."""
+    n = 2500
+    ctx = G.Context(0)
+    A = _spd(n, seed=11)
+    dA, info = _dev_potrf(ctx, A)
+    B = np.random.default_rng(2).random((n, 2))
+    outs = []
+    for _ in range(5):
+        dB = ctx.colmajor(B)
+        assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                          ctypes.c_void_p(dB.data_ptr()), 2, n) == 0
+        outs.append(ctx.host(dB))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    Xo = O.cho_solve_upper(sla.cholesky(A, lower=False), B)
+    assert relnorm(outs[0], Xo) < 1e-11
 
 
 @pytest.mark.parametrize("n", [100, 300, 513])

@@ -39,7 +39,30 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP64_MFMA_PEAK = 78.6      # TFLOP/s, FP64 matrix spec (measured 77.5 in tools/probe)
+FP64_MFMA_PEAK = 78.6      # TFLOP/s, FP64 matrix spec (measured 77.7 in tools/probe)
+DOMINANT_KERNEL = "gemm_tn_pipe8_kernel"
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+
+
+def pmc_traffic(kernel, n, npred):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc_summary.json, written by tools/profile_round.sh from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command, FETCH_SIZE
+    doubled per the gfx950 16-B/lane correction).  None when no summary matches."""
+    try:
+        files = sorted(f for f in os.listdir(PROFILES) if f.endswith("_pmc_summary.json"))
+    except OSError:
+        return None
+    for f in reversed(files):
+        try:
+            with open(os.path.join(PROFILES, f)) as fh:
+                js = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        k = js.get("kernels", {}).get(kernel)
+        if k and js.get("config", {}).get("N") == n and js.get("config", {}).get("np") == npred:
+            return k.get("traffic_bytes_per_launch")
+    return None
 
 
 def parse():
@@ -212,19 +235,18 @@ def main():
     for i, nm in enumerate(names):
         stg[nm] = e[i].elapsed_time(e[i + 1])
     cls = {}
-    for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other"]):
+    for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other", "gemm_pipe"]):
         ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
         lib.gpr_timing_get(ctx.h, c, ctypes.byref(ms), ctypes.byref(ln), ctypes.byref(fl))
         cls[nm] = (ms.value, ln.value, fl.value)
     kb_ms = cls["kbuild"][0]
     kbuild_gbs = 8.0 * N * N / (kb_ms * 1e-3) / 1e9
     potrf_tf = (N ** 3 / 3.0) / (stg["potrf"] * 1e-3) / 1e12
-    # dominant kernel: gemm_tn_kernel = classes syrk + panel GEMMs + trsm_gemm (+ others not
-    # counted); timed per launch.  Panel class also holds the diag kernels (flops 0).
-    g_ms = cls["syrk"][0] + cls["trsm_gemm"][0]
-    g_launch = cls["syrk"][1] + cls["trsm_gemm"][1]
-    g_fl = cls["syrk"][2] + cls["trsm_gemm"][2]
+    # dominant kernel: gemm_tn_pipe8_kernel (POTRF trailing SYRK, TRSM trailing updates),
+    # timed per launch with HIP events on the stream it is launched on (timing class 5)
+    g_ms, g_launch, g_fl = cls["gemm_pipe"]
     achieved = g_fl / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
+    traffic = pmc_traffic(DOMINANT_KERNEL, N, NP)
 
     out = None
     if rank == 0:
@@ -251,13 +273,13 @@ def main():
             "stage_ms": stg,
             "syrk_TFLOPs": cls["syrk"][2] / (cls["syrk"][0] * 1e-3) / 1e12 if cls["syrk"][0] else None,
             "roofline": {
-                "kernel": "gemm_tn_kernel (POTRF trailing SYRK + posterior TRSM GEMMs)",
+                "kernel": DOMINANT_KERNEL,
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": FP64_MFMA_PEAK,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK,
-                "traffic": None,
+                "traffic": traffic,
                 "launches": g_launch,
                 "avg_launch_us": g_ms * 1e3 / max(g_launch, 1),
                 "flops_per_launch": g_fl / max(g_launch, 1),

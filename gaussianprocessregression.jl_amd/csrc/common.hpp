@@ -27,7 +27,11 @@ struct KParams {
   double l[KMAXP][KMAXD];        // inverse length-scales (multipliers) per SE part
 };
 
-enum TimingClass { TC_KBUILD = 0, TC_SYRK = 1, TC_PANEL = 2, TC_TRSM_GEMM = 3, TC_OTHER = 4, TC_N = 5 };
+// TC_GEMM_PIPE is kernel-level (every launch of the pipelined 2-WG/CU GEMM, whatever its call
+// site), recorded in addition to the call-site class.
+enum TimingClass {
+  TC_KBUILD = 0, TC_SYRK = 1, TC_PANEL = 2, TC_TRSM_GEMM = 3, TC_OTHER = 4, TC_GEMM_PIPE = 5, TC_N = 6
+};
 
 struct TimedLaunch {
   int cls;
@@ -76,9 +80,9 @@ struct gpr_ctx {
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> event_pool;
-  double t_ms[TC_N] = {0, 0, 0, 0, 0};
-  long long t_launches[TC_N] = {0, 0, 0, 0, 0};
-  double t_flops[TC_N] = {0, 0, 0, 0, 0};
+  double t_ms[TC_N] = {};
+  long long t_launches[TC_N] = {};
+  double t_flops[TC_N] = {};
 };
 
 // ---- error helpers -------------------------------------------------------------------

@@ -494,8 +494,10 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   const bool long_k = pipe_mode == 1 || (pipe_mode == 3 && g.K >= 2048);
   if (pipe && long_k)
     gemm_tn_pipe16_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
-  else if (pipe)
+  else if (pipe) {
+    TimerScope tk(ctx, TC_GEMM_PIPE, flops);
     gemm_tn_pipe8_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
+  }
   else if (vec)
     gemm_tn_kernel<true><<<(unsigned)nblk, 256, pad, ctx->ls>>>(a);
   else

@@ -70,11 +70,13 @@ int gpr_upload(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes);   /* sy
 int gpr_download(gpr_ctx_t ctx, void* dst, const void* src, size_t bytes); /* sync D2H */
 /* Inner panel width of the blocked factorisations: 64 or 128 (default 128). */
 int gpr_set_block(gpr_ctx_t ctx, int nb);
-/* Outer panel width = K of the big MFMA trailing updates (default 512, multiple of nb). */
+/* Outer panel width = K of the big MFMA trailing updates (default 1024, multiple of nb). */
 int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
 /* Per-kernel-class timing with HIP events on the context stream (bench instrumentation).
  * class: 0 K-assembly, 1 POTRF trailing update (SYRK), 2 POTRF panel (diag+TRSM),
- *        3 TRSM trailing GEMM, 4 other.  Returns accumulated ms, launch count, flops. */
+ *        3 TRSM trailing GEMM, 4 other (call-site classes), 5 every launch of the
+ *        pipelined MFMA GEMM kernel (kernel-level, overlaps 1-4).
+ *        Returns accumulated ms, launch count, flops (bytes for class 0). */
 int gpr_timing_enable(gpr_ctx_t ctx, int on);
 int gpr_timing_get(gpr_ctx_t ctx, int cls, double* ms, long long* launches, double* flops);
 int gpr_timing_reset(gpr_ctx_t ctx);

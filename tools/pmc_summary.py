@@ -1,0 +1,67 @@
+"""Summarise a round's rocprofv3 passes of bench.py into profiles/rNN_pmc_summary.json.
+
+Inputs (written by tools/profile_round.sh): <dir>/fetch/**/*counter_collection.csv and
+<dir>/write/**/*counter_collection.csv (one --pmc pass each) and <dir>/trace/**/*kernel_stats.csv.
+Per kernel name: mean FETCH_SIZE and WRITE_SIZE per dispatch (rocprofv3 reports KiB),
+FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests of 16-B/lane
+streaming reads at 64 B), plus the kernel-trace average duration."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    s = name.replace("(anonymous namespace)::", "").strip()
+    if s.startswith("void "):
+        s = s[5:]
+    return s.split("(")[0].split("<")[0].split("::")[-1].strip()
+
+
+def per_dispatch(pattern, counter):
+    tot, cnt = defaultdict(float), defaultdict(set)
+    for f in glob.glob(pattern, recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = short(r["Kernel_Name"])
+            tot[name] += float(r["Counter_Value"])
+            cnt[name].add(r["Dispatch_Id"])
+    return {k: tot[k] / max(len(cnt[k]), 1) for k in tot}, {k: len(v) for k, v in cnt.items()}
+
+
+def trace_stats(pattern):
+    out = {}
+    for f in glob.glob(pattern, recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = short(r["Name"])
+            out[name] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                         "total_ms": float(r["TotalDurationNs"]) / 1e6}
+    return out
+
+
+def main():
+    d, n, npred = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    fetch, nf = per_dispatch(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
+    write, nw = per_dispatch(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
+    stats = trace_stats(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        fb = 2.0 * fetch.get(k, 0.0) * 1024.0
+        wb = write.get(k, 0.0) * 1024.0
+        kernels[k] = {"dispatches_fetch_pass": nf.get(k, 0), "dispatches_write_pass": nw.get(k, 0),
+                      "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                      "traffic_bytes_per_launch": fb + wb, "trace": stats.get(k)}
+    out = {"config": {"N": n, "np": npred},
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
+                     "`bench.py --steps 1 --warmup 0 --no-cpu-baseline`; FETCH_SIZE x2 (gfx950 "
+                     "16-B/lane correction), KiB -> bytes; WRITE_SIZE of 8-B/lane stores is "
+                     "uncalibrated (MI355X_MICROARCH.md, HBM section)",
+           "kernels": kernels}
+    json.dump(out, sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main()

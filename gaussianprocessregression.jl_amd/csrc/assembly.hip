@@ -12,11 +12,28 @@
 // computed; each is stored directly and, transposed through LDS, as its mirror tile, so
 // every N^2 element is written exactly once with 512-B coalesced column segments and the
 // exp work is halved.
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
 
 constexpr int KT = 64;  // output tile edge
+
+// 16-B stores need a 16-B aligned K and an even leading dimension (GPR_KBUILD_SCALAR forces
+// the 8-B-store kernels, for A/B runs)
+// persistent grid of the 16-B-store kernels: workgroups per CU x 256 CUs (GPR_KBUILD_WGS)
+inline long long kbuild_grid() {
+  static const long long g = 256LL * (getenv("GPR_KBUILD_WGS") ? atoi(getenv("GPR_KBUILD_WGS")) : 8);
+  return g;
+}
+
+inline bool vec_store_ok(const double* K, int ldk) {
+  static const bool off = getenv("GPR_KBUILD_SCALAR") != nullptr;
+  return !off && ((uintptr_t)K & 15) == 0 && (ldk & 1) == 0;
+}
 
 // xs[p][k + a*d] = x[k + a*d] * l_p[k]   (x .* ls[:, n], src/covariance.jl:90)
 __global__ void scale_inputs_kernel(KParams kp, const double* __restrict__ X, int n,
@@ -30,6 +47,42 @@ __global__ void scale_inputs_kernel(KParams kp, const double* __restrict__ X, in
     const int k = (int)(r % d);
     xs[t] = X[r] * kp.l[p][k];
   }
+}
+
+// exp(-D) of the assembly kernels.  GPR_KBUILD_NOEXP (tools/kbuild_bench_noexp only, never
+// the library) swaps in a cheap stand-in to separate exp cost from store cost.
+__device__ __forceinline__ double kexp_neg(double dist) {
+#ifdef GPR_KBUILD_NOEXP
+  return fma(dist, -1e-3, 1.0);
+#else
+  return exp(-1.0 * dist);
+#endif
+}
+
+// exp(-dist) for the 16-B-store kernels: Tang's table method, ~1 ulp (the ocml exp costs ~28
+// instructions with its range checks and quarter-rate conversions and made K-assembly
+// VALU-bound at two SE parts).  x = -dist clamped at -800 (exp underflows to 0 long before;
+// a NaN dist fails the compare and propagates), n = rint(x 256/ln2), r = x - n ln2/256 in two
+// Cody-Waite steps (n L1 exact: L1 has 32 significant bits, |n| < 2^19), |r| <= ln2/512,
+// exp(x) = 2^(n>>8) T[n&255] (1 + r p(r)) with a degree-5 Taylor p (truncation < 1e-20) and
+// T[j] = 2^(j/256) rounded once from extended precision on the host (ctx->dexptab).
+__device__ __forceinline__ double kexp_neg_tab(double dist, const double* tab) {
+#ifdef GPR_KBUILD_NOEXP
+  (void)tab;
+  return fma(dist, -1e-3, 1.0);
+#else
+  const double x = dist > 800.0 ? -800.0 : -dist;
+  const double nf = __builtin_rint(x * 369.3299304675746);
+  double r = fma(nf, -0.00270760617331689, x);
+  r = fma(nf, -7.453964567463233e-13, r);
+  const int ni = (int)nf;
+  double p = fma(r, 0.008333333333333333, 0.041666666666666664);
+  p = fma(r, p, 0.16666666666666666);
+  p = fma(r, p, 0.5);
+  p = fma(r, p, 1.0);
+  const double t = tab[ni & 255];
+  return __builtin_ldexp(fma(t, r * p, t), ni >> 8);
+#endif
 }
 
 // D = sum_k (xr_k - xc_k)^2 with xr in registers and xc wave-uniform (scalar loads).
@@ -94,7 +147,7 @@ __global__ __launch_bounds__(256) void kmat_sym_kernel(KParams kp, const double*
         } else {
           dist = sqdist<0>(xrow, xc, d);
         }
-        double t = s2 * exp(-1.0 * dist);
+        double t = s2 * kexp_neg(dist);
         if (i == j) t += kp.eps;
         vals[c] = (p == 0) ? t : vals[c] + t;
       }
@@ -161,7 +214,7 @@ __global__ __launch_bounds__(256) void kmat_cross_kernel(KParams kp, const doubl
         } else {
           dist = sqdist<0>(xrow, xc, d);
         }
-        const double t = s2 * exp(-1.0 * dist);
+        const double t = s2 * kexp_neg(dist);
         vals[c] = (p == 0) ? t : vals[c] + t;
       }
     }
@@ -255,10 +308,183 @@ int scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, doubl
   return 0;
 }
 
+// ---- 16-B-store assembly (compile-time d, 16-B aligned K with even ldk) ----------------
+// Thread t of the 256 owns rows i0 + 2 (t & 31) + {0,1} and columns j0 + (t >> 5) + 8c,
+// c < 8: every direct store is one 16-B pair of adjacent rows (32 lanes = one 512-B column
+// segment).  Row features stay in registers; the tile's 64 column points sit in LDS and are
+// read as half-wave broadcasts.  The mirror tile goes through LDS (row stride 65 doubles:
+// conflict-free scalar writes) and is re-read as row pairs, so it too is stored 16 B/lane.
+constexpr int KT_LDS = KT * (KT + 1);  // doubles; also holds the 64 x D column points
+
+template <int D, bool SYM>
+__device__ __forceinline__ void kmat_tile_compute(const KParams& kp, const double* __restrict__ xs,
+                                                  int n, const double* __restrict__ xcs, int m,
+                                                  int i0, int j0, double* lds, const double* etab,
+                                                  double (&v)[8][2]) {
+  constexpr int NFILL = (KT * D + 255) / 256;  // column-point doubles per thread per part
+  const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
+  const int ia = min(i0 + 2 * l32, n - 1), ib = min(i0 + 2 * l32 + 1, n - 1);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c][0] = v[c][1] = 0.0;
+  for (int p = 0; p < kp.nse; ++p) {
+    const double* xp_rows = xs + (size_t)p * n * D;
+    const double* xp_cols = xcs + (size_t)p * m * D;
+    // all global loads of this part first (row features + this thread's column-point share)
+    double xr0[D], xr1[D], fill[NFILL];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xr0[k] = xp_rows[(size_t)ia * D + k];
+      xr1[k] = xp_rows[(size_t)ib * D + k];
+    }
+#pragma unroll
+    for (int f = 0; f < NFILL; ++f) {
+      const int e = t + 256 * f;
+      const int jl = e / D;
+      fill[f] = e < KT * D ? xp_cols[(size_t)min(j0 + jl, m - 1) * D + (e - jl * D)] : 0.0;
+    }
+    __syncthreads();  // previous part's column points fully consumed
+#pragma unroll
+    for (int f = 0; f < NFILL; ++f)
+      if (t + 256 * f < KT * D) lds[t + 256 * f] = fill[f];
+    __syncthreads();
+    // 16 independent distance accumulators (8 columns x 2 rows), k outermost
+    double d0[8], d1[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) d0[c] = d1[c] = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const double cv = lds[(cg + 8 * c) * D + k];
+        const double q0 = xr0[k] - cv, q1 = xr1[k] - cv;
+        d0[c] = fma(q0, q0, d0[c]);
+        d1[c] = fma(q1, q1, d1[c]);
+      }
+    }
+    const double s2 = kp.sigma[p] * kp.sigma[p];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      double t0 = s2 * kexp_neg_tab(d0[c], etab), t1 = s2 * kexp_neg_tab(d1[c], etab);
+      if (SYM) {
+        const int j = j0 + cg + 8 * c, i = i0 + 2 * l32;
+        if (i == j) t0 += kp.eps;
+        if (i + 1 == j) t1 += kp.eps;
+      }
+      v[c][0] = (p == 0) ? t0 : v[c][0] + t0;
+      v[c][1] = (p == 0) ? t1 : v[c][1] + t1;
+    }
+  }
+  if (SYM && kp.has_noise) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = j0 + cg + 8 * c, i = i0 + 2 * l32;
+      if (i == j) v[c][0] += kp.noise2;
+      if (i + 1 == j) v[c][1] += kp.noise2;
+    }
+  }
+}
+
+typedef double kd2 __attribute__((ext_vector_type(2)));
+
+// K is written once and not re-read by this kernel: non-temporal (streaming) stores
+__device__ __forceinline__ void store_pair(double* K, size_t idx, bool ok0, bool ok1, double a,
+                                           double b) {
+#ifdef GPR_KBUILD_NOSTORE  // diagnostics (tools/kbuild_bench_nostore): compute-only timing
+  if (!(a == a) || !(b == b)) K[idx] = a;
+  return;
+#endif
+  if (ok1) {
+#ifdef GPR_KBUILD_TEMPORAL
+    *reinterpret_cast<kd2*>(K + idx) = kd2{a, b};
+#else
+    __builtin_nontemporal_store(kd2{a, b}, reinterpret_cast<kd2*>(K + idx));
+#endif
+  } else if (ok0) {
+    K[idx] = a;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void kmat_sym2_kernel(KParams kp, const double* __restrict__ xs,
+                                                        int n, double* __restrict__ K, size_t ldk,
+                                                        int ntiles) {
+  __shared__ double lds[KT_LDS];
+  __shared__ double etab[256];
+  const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
+  etab[t] = kp.exptab[t];
+  __syncthreads();
+  // persistent: a workgroup walks tiles, so one tile's math overlaps the previous tile's
+  // stores draining to HBM
+  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+    int bj = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+    while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
+    while (bj * (bj + 1) / 2 > bid) --bj;
+    const int bi = bid - bj * (bj + 1) / 2;
+    const int i0 = bi * KT, j0 = bj * KT;
+    double v[8][2];
+    kmat_tile_compute<D, true>(kp, xs, n, xs, n, i0, j0, lds, etab, v);
+    const int i = i0 + 2 * l32;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = j0 + cg + 8 * c;
+      if (j < n) store_pair(K, (size_t)i + (size_t)j * ldk, i < n, i + 1 < n, v[c][0], v[c][1]);
+    }
+    if (bi == bj) continue;
+    __syncthreads();  // column points no longer needed: reuse LDS for the transpose
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int jl = cg + 8 * c;
+      lds[(2 * l32) * (KT + 1) + jl] = v[c][0];
+      lds[(2 * l32 + 1) * (KT + 1) + jl] = v[c][1];
+    }
+    __syncthreads();
+    // mirror: K[j0 + 2q + {0,1}, i0 + il] = tile[il][2q + {0,1}]
+    const int jj = j0 + 2 * l32;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int il = cg + 8 * c;
+      if (i0 + il < n)
+        store_pair(K, (size_t)jj + (size_t)(i0 + il) * ldk, jj < n, jj + 1 < n,
+                   lds[il * (KT + 1) + 2 * l32], lds[il * (KT + 1) + 2 * l32 + 1]);
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void kmat_cross2_kernel(KParams kp, const double* __restrict__ xs,
+                                                          int n, const double* __restrict__ xps,
+                                                          int m, double* __restrict__ K,
+                                                          size_t ldk, int ntile_i, int ntiles) {
+  __shared__ double lds[KT * D];
+  __shared__ double etab[256];
+  const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
+  etab[t] = kp.exptab[t];
+  __syncthreads();
+  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+    const int bi = bid % ntile_i, bj = bid / ntile_i;
+    const int i0 = bi * KT, j0 = bj * KT;
+    double v[8][2];
+    kmat_tile_compute<D, false>(kp, xs, n, xps, m, i0, j0, lds, etab, v);
+    const int i = i0 + 2 * l32;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = j0 + cg + 8 * c;
+      if (j < m) store_pair(K, (size_t)i + (size_t)j * ldk, i < n, i + 1 < n, v[c][0], v[c][1]);
+    }
+  }
+}
+
 template <int D>
 void launch_sym(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk) {
   const int nt = (n + KT - 1) / KT;
   const long long nblk = (long long)nt * (nt + 1) / 2;
+  if constexpr (D > 0) {
+    if (vec_store_ok(K, ldk)) {
+      const int grid = (int)std::min<long long>(nblk, kbuild_grid());
+      kmat_sym2_kernel<D><<<grid, 256, 0, ctx->stream>>>(kp, xs, n, K, (size_t)ldk, (int)nblk);
+      return;
+    }
+  }
   kmat_sym_kernel<D><<<(unsigned)nblk, 256, 0, ctx->stream>>>(kp, xs, n, K, (size_t)ldk);
 }
 
@@ -266,8 +492,16 @@ template <int D>
 void launch_cross(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const double* xps,
                   int m, double* K, int ldk) {
   const int nti = (n + KT - 1) / KT, ntj = (m + KT - 1) / KT;
-  kmat_cross_kernel<D><<<(unsigned)((long long)nti * ntj), 256, 0, ctx->stream>>>(
-      kp, xs, n, xps, m, K, (size_t)ldk, nti);
+  const unsigned nblk = (unsigned)((long long)nti * ntj);
+  if constexpr (D > 0) {
+    if (vec_store_ok(K, ldk)) {
+      const int grid = (int)std::min<long long>(nblk, kbuild_grid());
+      kmat_cross2_kernel<D><<<grid, 256, 0, ctx->stream>>>(kp, xs, n, xps, m, K, (size_t)ldk, nti,
+                                                           (int)nblk);
+      return;
+    }
+  }
+  kmat_cross_kernel<D><<<nblk, 256, 0, ctx->stream>>>(kp, xs, n, xps, m, K, (size_t)ldk, nti);
 }
 
 #define DISPATCH_D(FN, ...)                 \

@@ -25,6 +25,7 @@ struct KParams {
   double sigma[KMAXP];           // sigma of each SE part
   int hp_off[KMAXP];             // flat hp index of each SE part's sigma
   double l[KMAXP][KMAXD];        // inverse length-scales (multipliers) per SE part
+  const double* exptab;          // device table 2^(j/256), j < 256 (ctx->dexptab)
 };
 
 // TC_GEMM_PIPE is kernel-level (every launch of the pipelined 2-WG/CU GEMM, whatever its call
@@ -64,6 +65,7 @@ struct gpr_ctx {
   bool fac_valid = false;
 
   int* dinfo = nullptr;         // device info word
+  double* dexptab = nullptr;    // 2^(j/256), j < 256, correctly rounded (assembly exp)
   double* dscratch = nullptr;   // generic scratch (partials, small vectors)
   size_t scratch_cap = 0;       // doubles
   double* dbig = nullptr;       // large scratch (Z for potri, Kpx for predict, ...)

@@ -1,4 +1,5 @@
 // Context, memory, error and timing plumbing of libgpr_hip.so.
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -89,6 +90,7 @@ int make_kparams(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d
   if (!hp) return set_err(ctx, GPR_E_ARG, "hp is NULL");
   if (d <= 0 || d > KMAXD) return set_err(ctx, GPR_E_UNSUP, "d=%d unsupported (1..%d)", d, KMAXD);
   memset(kp, 0, sizeof *kp);
+  kp->exptab = ctx->dexptab;
   kp->d = d;
   kp->eps = eps;
   int off = 0;
@@ -182,6 +184,17 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     delete ctx;
     return GPR_E_NOMEM;
   }
+  {
+    // 2^(j/256) in extended precision, rounded once to double (assembly kexp_neg table)
+    double tab[256];
+    for (int j = 0; j < 256; ++j) tab[j] = (double)exp2l((long double)j / 256.0L);
+    if (hipMalloc((void**)&ctx->dexptab, sizeof tab) != hipSuccess ||
+        hipMemcpy(ctx->dexptab, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(ctx->dinfo);
+      delete ctx;
+      return GPR_E_NOMEM;
+    }
+  }
   *out = ctx;
   return 0;
 }
@@ -197,6 +210,7 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->smain) hipStreamDestroy(ctx->smain);
   if (ctx->winv) hipFree(ctx->winv);
   if (ctx->dinfo) hipFree(ctx->dinfo);
+  if (ctx->dexptab) hipFree(ctx->dexptab);
   if (ctx->dscratch) hipFree(ctx->dscratch);
   if (ctx->dbig) hipFree(ctx->dbig);
   if (ctx->dbig2) hipFree(ctx->dbig2);

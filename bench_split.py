@@ -1,0 +1,117 @@
+"""C5 benchmark: split-kernel block prediction sharded over GPUs (BASELINE
+config 5).  Secondary to bench.py (the driver's headline line); same launch conventions:
+
+  python bench_split.py [--steps K --warmup W]                           # 1 GPU
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench_split.py --gpus N                            # N GPUs (RCCL)
+
+Workload (synthetic, seeded): ns = 32768 training points, d = 8, SE+WN, test grid
+x_{e,q} = xe_e + xq_q with ne = nq = 1024 (1,048,576 test points).  One step = the whole
+job: fit on rank 0 (K, POTRF, wt; or on every rank with --fit replicate), broadcast of
+U (8N^2 bytes) and wt over RCCL, each rank's grid rows (mean for all of them, diagonal
+variance for its share of the first --var-rows rows), all_gather to every rank in the
+reference layouts.  Scaling is strong (fixed total work).  value = test points per second
+for the whole job.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gaussianprocessregression.jl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--ns", type=int, default=32768)
+    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--ne", type=int, default=1024)
+    ap.add_argument("--nq", type=int, default=1024)
+    ap.add_argument("--var-rows", type=int, default=32)
+    ap.add_argument("--fit", default="broadcast", choices=["broadcast", "replicate"])
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    import gpr_amd as G
+    from gpr_amd.distributed import split_predict_distributed
+
+    ctx = G.Context(local)
+    d = a.d
+    x = np.random.default_rng(0).random((d, a.ns))
+    y = np.sin(x.sum(0)) ** 2
+    xe = np.random.default_rng(2).random((d, a.ne))
+    xq = np.random.default_rng(3).random((d, a.nq))
+    hp = np.r_[1.0, [3.0 * math.sqrt(8.0 / d)] * d, 0.1]
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=ctx)
+    cm = G.Cmap("+", xe, xq)
+    vr = (1, a.var_rows) if a.var_rows > 0 else None
+
+    def step():
+        return split_predict_distributed(md, cm, var_range=vr, fit=a.fit)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        mu, var = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = (time.perf_counter() - t0) / a.steps
+    tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    npts = a.ne * a.nq
+    mean_flops = 2.0 * a.ne * a.ns * a.nq
+    var_flops = float(a.nq) * a.ns * a.ns * (a.var_rows if vr else 0)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "split-predict test points/s (C5: mean + diagonal var rows)",
+            "value": npts / dt,
+            "unit": "test points/s (whole job)",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (x, xe, xq ~ U[0,1) seeded, y = sin(sum x)^2)",
+            "config": {"workload": f"C5 split predict SE+WN ns={a.ns} d={d} ne={a.ne} nq={a.nq} "
+                                   f"var_rows={a.var_rows} fit={a.fit}",
+                       "parallelism": f"e-row shards x{world}, RCCL broadcast + all_gather"},
+            "algorithmic_tflop_per_step": (mean_flops + var_flops) / 1e12,
+            "results_finite": bool(np.isfinite(mu).all() and np.isfinite(var).all()),
+        }), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

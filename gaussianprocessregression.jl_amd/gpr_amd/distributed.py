@@ -1,0 +1,148 @@
+"""Multi-GPU split-kernel block prediction: one process per GPU.
+
+The reference runs ``predict(md, Cmap(+, xe, xq); diagonal_var=true)``
+(src/predict.jl:14-25 -> src/split_predict.jl:5-53) on one CPU.  Here the e-rows of the
+test grid x_{e,q} = xe_e + xq_q are independent once the training factor U and the weights
+wt = K^{-1} y exist, so:
+
+  1. rank 0 fits: K, POTRF (U), wt                        (src/predict.jl:29-34)
+     fit="broadcast": U (N x N) and wt are broadcast from rank 0 over RCCL/xGMI;
+     fit="replicate": every rank factorises K itself (no N^2 exchange; the better choice
+     when the broadcast of 8N^2 bytes costs more than one K + POTRF on a GPU).
+  2. rank r takes grid rows [lo_r, hi_r) (balanced contiguous split of ne) and computes
+     its mean rows mu[lo:hi, :] and the variance rows of var_range that fall inside
+     (src/split_predict.jl:10-19, :39-53; var_range default 1:3,
+     src/caches/split_kernel.jl:10).  Rows outside var_range keep the prior.
+  3. the shards are all-gathered (mu: (hi-lo) x nq per rank, var: (hi-lo) nq) and
+     reassembled in the reference layouts: mu ne x nq column-major (linear e + q ne),
+     var.diag index e nq + q.
+
+The collective sequence (broadcast, then all_gather) is the only data exchange; the
+per-rank compute is a pluggable backend so the distributed logic is tested on CPU with
+gloo (tests/test_distributed.py) and runs on libgpr_hip.so with RCCL on the GPUs
+(HipSplitBackend, the default).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import core
+from ._lib import lib
+
+__all__ = ["shard_rows", "HipSplitBackend", "split_predict_distributed"]
+
+
+def shard_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Balanced contiguous partition of n rows: the first n % world ranks get one more."""
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def var_rows(var_range: Optional[Tuple[int, int]], ne: int) -> Tuple[int, int]:
+    """Julia 1-based inclusive var_range -> 0-based half-open [lo, hi) clamped to ne
+    (None = no variance rows)."""
+    if var_range is None:
+        return 0, 0
+    a, b = var_range
+    lo, hi = max(a, 1) - 1, min(b, ne)
+    return (lo, hi) if hi > lo else (0, 0)
+
+
+class HipSplitBackend:
+    """Per-rank compute on libgpr_hip.so (the product path).
+
+    fit():          gpr_fit -> (U, wt) device tensors (U column-major N x N).
+    empty_fit():    receive buffers for the broadcast.
+    predict_rows(): gpr_split_predict for grid rows [e_lo, e_hi) into full-layout device
+                    buffers (mu: nq x ne tensor = ne x nq column-major; var: ne nq).
+    """
+
+    def __init__(self, md: core.GPRModel, eps: float = core.EPS_DEFAULT):
+        if md.y.ndim != 1:
+            raise ValueError("split prediction needs a 1-D y (Diagonal(wt), src/split_predict.jl:13)")
+        self.md, self.eps, self.ctx = md, eps, md.ctx
+        self.device = self.ctx.device
+
+    def empty_fit(self):
+        n = self.md.n
+        return self.ctx.empty(n, n), self.ctx.empty(n)
+
+    def fit(self):
+        pc = core.GPRSplitPredictCache(self.md, 0, 0)
+        core._update_predict_cache(core.pc_adapter(pc), self.md, self.eps)
+        return pc.Kxx, pc.wt
+
+    def predict_rows(self, cm: core.Cmap, U, wt, e_lo: int, e_hi: int, v_lo: int, v_hi: int):
+        md, ctx = self.md, self.ctx
+        _, ne, nq = cm.shape
+        mu = ctx.zeros(nq, ne)
+        var = ctx.zeros(ne * nq)
+        kinds, nk = core._kinds_arr(md.covar)
+        _, hpp = core._hp_arr(md.params)
+        dxe, dxq = ctx.colmajor(cm.xe), ctx.colmajor(cm.xq)
+        ctx.check(lib.gpr_split_predict(ctx.h, kinds, nk, hpp, md.d, core._ptr(md.dx()), md.n,
+                                        core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
+                                        core._ptr(dxq), nq, e_lo, e_hi, v_lo, v_hi, self.eps,
+                                        core._ptr(mu), core._ptr(var)), "gpr_split_predict")
+        ctx.sync()
+        return mu, var
+
+
+def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
+                              var_range: Optional[Tuple[int, int]] = (1, 3),
+                              backend=None, fit: str = "broadcast", group=None,
+                              eps: float = core.EPS_DEFAULT):
+    """Sharded predict(md, Cmap(+, xe, xq); diagonal_var=true) over the ranks of `group`.
+
+    Every rank must call it with the same model and grid (SPMD).  Returns, on every rank,
+    (mu, var): mu as an ne x nq numpy array (Julia indexing; linear e + q ne) and var as
+    the length ne nq diagonal (index e nq + q), identical to the single-process result.
+    """
+    if fit not in ("broadcast", "replicate"):
+        raise ValueError("fit must be 'broadcast' or 'replicate'")
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    backend = backend or HipSplitBackend(md, eps)
+    _, ne, nq = cm.shape
+
+    # 1. factor + weights: rank 0 (broadcast) or every rank (replicate)
+    if fit == "broadcast":
+        if rank == 0:
+            U, wt = backend.fit()
+        else:
+            U, wt = backend.empty_fit()
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(U, src, group=group)
+        dist.broadcast(wt, src, group=group)
+    else:
+        U, wt = backend.fit()
+
+    # 2. this rank's grid rows and the var_range rows inside them
+    lo, hi = shard_rows(ne, world, rank)
+    v_lo, v_hi = var_rows(var_range, ne)
+    mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+
+    # 3. pack the shard, all-gather padded shards, reassemble the reference layouts
+    emax = -(-ne // world)
+    mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
+    var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
+    if hi > lo:
+        mu_sh[:, :hi - lo] = mu_full[:, lo:hi]
+        var_sh[:(hi - lo) * nq] = var_full[lo * nq:hi * nq]
+    mus = [torch.empty_like(mu_sh) for _ in range(world)]
+    vars_ = [torch.empty_like(var_sh) for _ in range(world)]
+    dist.all_gather(mus, mu_sh, group=group)
+    dist.all_gather(vars_, var_sh, group=group)
+    mu = np.empty((nq, ne))
+    var = np.empty(ne * nq)
+    for r in range(world):
+        a, b = shard_rows(ne, world, r)
+        if b > a:
+            mu[:, a:b] = mus[r][:, :b - a].cpu().numpy()
+            var[a * nq:b * nq] = vars_[r][:(b - a) * nq].cpu().numpy()
+    return mu.T.copy(), var

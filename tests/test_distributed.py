@@ -1,0 +1,160 @@
+"""Multi-process split prediction (gpr_amd.distributed) on CPU with gloo.
+
+The distributed logic under test is the product code: rank-0 fit + broadcast of (U, wt)
+(or replicated fits), balanced row sharding, var_range rows per shard, padded all_gather
+and reassembly into the reference layouts (mu ne x nq with linear e + q ne,
+src/split_predict.jl:10-19; var.diag index e nq + q, :39-53).  Only the per-rank compute
+is swapped for an oracle-backed CPU backend (test infrastructure), which fills the same
+full-layout buffers the HIP backend fills.  Expected results come from the single-process
+oracle split_predict.  A GPU test runs the real HIP backend over a 1-rank RCCL group.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import gpr_oracle as O
+
+gd = pytest.importorskip("gpr_amd.distributed")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _problem(ne=7, nq=5, ns=60, d=3, seed=4):
+    rng = np.random.default_rng(seed)
+    x = rng.random((d, ns))
+    y = np.sin(x.sum(0)) ** 2
+    xe, xq = 0.5 * rng.random((d, ne)), 0.5 * rng.random((d, nq))
+    kinds = ["SE", "WN"]
+    hp = O.default_hp(kinds, d, noise=0.05)
+    return kinds, hp, x, y, xe, xq
+
+
+class _Cmap:
+    def __init__(self, xe, xq):
+        self.xe, self.xq = xe, xq
+
+    @property
+    def shape(self):
+        return (self.xe.shape[0], self.xe.shape[1], self.xq.shape[1])
+
+
+class OracleBackend:
+    """CPU stand-in for HipSplitBackend (same buffers, same row/var-range semantics)."""
+
+    def __init__(self, kinds, hp, x, y, allow_fit=True):
+        self.kinds, self.hp, self.x, self.y, self.allow_fit = kinds, hp, x, y, allow_fit
+
+    def empty_fit(self):
+        n = self.x.shape[1]
+        return torch.empty(n, n, dtype=torch.float64), torch.empty(n, dtype=torch.float64)
+
+    def fit(self):
+        if not self.allow_fit:
+            raise AssertionError("this rank must receive U/wt by broadcast")
+        U = O.chol_upper(O.kernel(self.kinds, self.hp, self.x, None))
+        wt = O.cho_solve_upper(U, self.y)
+        return torch.from_numpy(np.ascontiguousarray(U.T)), torch.from_numpy(wt)  # column-major
+
+    def predict_rows(self, cm, U, wt, e_lo, e_hi, v_lo, v_hi):
+        _, ne, nq = cm.shape
+        Un, w = U.numpy().T, wt.numpy()
+        A, B, C = O.split_factors(self.kinds, self.hp, self.x, cm.xe, cm.xq)
+        mu = torch.zeros(nq, ne, dtype=torch.float64)
+        var = torch.zeros(ne * nq, dtype=torch.float64)
+        prior = O.diag_prior(self.kinds, self.hp, self.x.shape[0])
+        for e in range(e_lo, e_hi):
+            m = np.zeros(nq)
+            for k in range(A.shape[2]):
+                m += A[e, :, k] * (B[e, :, k] @ (w[:, None] * C[:, :, k]))
+            mu[:, e] = torch.from_numpy(m)
+            var[e * nq:(e + 1) * nq] = prior
+            if v_lo <= e < v_hi:
+                Kxq = sum(A[e, :, None, k] * B[e, None, :, k] * C[:, :, k].T for k in range(A.shape[2]))
+                V = sla.solve_triangular(Un, Kxq.T, trans="T", lower=False).T
+                var[e * nq:(e + 1) * nq] = torch.from_numpy(prior - np.sum(V * V, axis=1))
+        return mu, var
+
+
+def _worker(rank, world, port, out, ne, nq, var_range, fit):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kinds, hp, x, y, xe, xq = _problem(ne=ne, nq=nq)
+        be = OracleBackend(kinds, hp, x, y, allow_fit=(fit == "replicate" or rank == 0))
+        mu, var = gd.split_predict_distributed(None, _Cmap(xe, xq), var_range=var_range,
+                                               backend=be, fit=fit)
+        np.save(os.path.join(out, f"mu{rank}.npy"), mu)
+        np.save(os.path.join(out, f"var{rank}.npy"), var)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,ne,nq,var_range,fit", [
+    (2, 7, 5, (1, 3), "broadcast"),     # reference default var_range, ragged shards
+    (3, 8, 4, (1, 8), "replicate"),     # full var_range, replicated factorisation
+    (2, 9, 3, (3, 7), "broadcast"),     # var_range straddling the shard boundary
+    (3, 2, 6, (1, 3), "broadcast"),     # more ranks than rows: an empty shard
+])
+def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit):
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path), ne, nq, var_range, fit), nprocs=world,
+             join=True)
+    kinds, hp, x, y, xe, xq = _problem(ne=ne, nq=nq)
+    mu_o, var_o = O.split_predict(kinds, hp, x, y, xe, xq, var_range=var_range)
+    for r in range(world):  # every rank holds the full result
+        mu = np.load(tmp_path / f"mu{r}.npy")
+        var = np.load(tmp_path / f"var{r}.npy")
+        assert mu.shape == (ne, nq)
+        np.testing.assert_allclose(mu, mu_o, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(var, var_o, rtol=1e-12, atol=1e-14)
+
+
+def test_shard_rows_partition():
+    for n in range(0, 40):
+        for world in range(1, 9):
+            parts = [gd.shard_rows(n, world, r) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[r][1] == parts[r + 1][0] for r in range(world - 1))
+            sizes = [b - a for a, b in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_var_rows_conversion():
+    assert gd.var_rows((1, 3), 10) == (0, 3)        # Julia 1:3 -> [0, 3)
+    assert gd.var_rows((1, 3), 2) == (0, 2)         # clamped to ne
+    assert gd.var_rows(None, 5) == (0, 0)
+    assert gd.var_rows((4, 3), 5) == (0, 0)         # empty range
+
+
+@pytest.mark.gpu
+def test_split_predict_distributed_hip_single_rank():
+    """The HIP backend through the real collective path (1-rank RCCL group) equals the
+    single-process split predict."""
+    G = pytest.importorskip("gpr_amd")
+    if dist.is_initialized():
+        pytest.skip("process group already initialised")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        kinds, hp, x, y, xe, xq = _problem(ne=11, nq=13, ns=300, d=4)
+        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+        cm = G.Cmap("+", xe, xq)
+        for fit in ("broadcast", "replicate"):
+            mu, var = gd.split_predict_distributed(md, cm, var_range=(1, 11), fit=fit)
+            mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 11))
+            np.testing.assert_allclose(mu, mu1, rtol=1e-14, atol=0)
+            np.testing.assert_allclose(var, var1, rtol=1e-14, atol=0)
+        mu_o, var_o = O.split_predict(kinds, hp, x, y, xe, xq, var_range=(1, 11))
+        np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+    finally:
+        dist.destroy_process_group()

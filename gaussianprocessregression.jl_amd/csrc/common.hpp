@@ -72,6 +72,14 @@ struct gpr_ctx {
   size_t big_cap = 0;           // doubles
   double* dbig2 = nullptr;
   size_t big2_cap = 0;
+  int panel_sq = 0;             // square-panel factorisation (1 launch + 1 GEMM per panel;
+                                // GPR_PANEL_SQ=1; slower than per-block panels so far)
+  int* dsync = nullptr;         // inter-workgroup counters of the square-panel kernel
+  double* dsqinv = nullptr;     // U_sq^{-1} of every outer panel square (nb2^2 per slot)
+  size_t sqinv_cap = 0;         // doubles
+  int sqinv_nb2 = 0;            // nb2 the slots were written with (0 = none valid)
+  double* dpanel = nullptr;     // out-of-place result of the panel's rest GEMM
+  size_t panel_cap = 0;
   double* dtrsv = nullptr;      // single-launch triangular sweep hand-off vector (n x 2)
   size_t trsv_cap = 0;
   double* dxs = nullptr;        // per-part scaled training inputs  (nse x d x n)
@@ -136,7 +144,8 @@ struct GemmArgs {
   int mask_upper;         // element mask m <= n + mask_off on a general grid
   int mask_off;           // column offset of C relative to its row origin (mask_upper)
   int kfrom_n;            // tile's K loop starts at its n0 (triangular factor, Z^T Z)
-  int kmax_from_n;        // tile's K loop ends at min(K, n0+TN) (lower-triangular RHS)
+  int kend_from_m;        // tile's K loop ends at min(K, m0+TM) (upper-triangular P:
+                          // P[t][m] = 0 for t > m, e.g. P = U^{-1})
   const double* qscale;   // optional per-k scale of Q (diag(wt) C)
   const double* E; int lde;  // optional Hadamard factor: C = beta*C + alpha*acc*E
   double* norm_out;       // optional: norm_out[n] -= sum_m (result)^2 (needs M <= tile)

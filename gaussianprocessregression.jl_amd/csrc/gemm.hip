@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
   const int wm = w & 1, wn = w >> 1;
 
   const int kbeg = g.kfrom_n ? n0 : 0;
-  const int kend = g.K;
+  const int kend = g.kend_from_m ? min(g.K, m0 + TM) : g.K;
   const int nst = kend > kbeg ? (kend - kbeg + TK - 1) / TK : 0;
 
   d4 acc[4][4];
@@ -316,7 +316,7 @@ __device__ __forceinline__ void gemm_tn_pipe_body(const GemmK& a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w & 1, wn = w >> 1;
   const int kbeg = g.kfrom_n ? n0 : 0;
-  const int nst = (g.K - kbeg) / TKS;
+  const int nst = ((g.kend_from_m ? min(g.K, m0 + TM) : g.K) - kbeg) / TKS;
 
   // DMA sources: instruction r of wave w fills rows ROWS_PER_DMA (4r + w) + (L / NCH); lane
   // L lands at physical chunk L % NCH of its row, so it fetches the logical chunk
@@ -473,6 +473,8 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   } else {
     nblk = (long long)a.super_m * super_n * a.gm * a.gn;
     flops = 2.0 * g.M * (double)g.N * g.K;
+    if (g.kend_from_m)  // upper-triangular P: row m of the product uses K-range [0, m]
+      flops = (double)g.N * g.M * (g.M + 1);
     if (g.mask_upper) {  // exclude the masked corner rows m > n + mask_off
       const double rows_below = std::max(0.0, (double)g.M - g.mask_off);
       const double cut = std::min(rows_below, (double)g.N);

@@ -152,6 +152,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   }
   if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
   if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
+  if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
   // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is
   // on the critical path of the lookahead chain.  GEMM streams get the complement mask.
@@ -215,6 +216,9 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dbig) hipFree(ctx->dbig);
   if (ctx->dbig2) hipFree(ctx->dbig2);
   if (ctx->dtrsv) hipFree(ctx->dtrsv);
+  if (ctx->dsync) hipFree(ctx->dsync);
+  if (ctx->dsqinv) hipFree(ctx->dsqinv);
+  if (ctx->dpanel) hipFree(ctx->dpanel);
   if (ctx->dxs) hipFree(ctx->dxs);
   if (ctx->dxps) hipFree(ctx->dxps);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);

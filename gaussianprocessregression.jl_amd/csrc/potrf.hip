@@ -76,11 +76,9 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 }
 
 template <int NB>
-__global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __restrict__ A,
-                                                                  size_t lda, int n, int kglob,
-                                                                  int* __restrict__ info,
-                                                                  double* __restrict__ winv,
-                                                                  int mode) {
+__device__ __forceinline__ void diag_block_body(double* __restrict__ A, size_t lda, int n,
+                                                int kglob, int* __restrict__ info,
+                                                double* __restrict__ winv, int mode, int blk) {
   constexpr int SB = 32, NSB = NB / SB, NW = DIAG_THREADS / 64;
   constexpr int PK = NB * (NB + 1) / 2;
   constexpr int PER = NB * NB / DIAG_THREADS;  // elements per thread in the bulk copies
@@ -102,9 +100,9 @@ __global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __r
     k0 = kglob;
     kb = min(NB, n - kglob);
   } else {
-    k0 = blockIdx.x * NB;
+    k0 = blk * NB;
     kb = min(NB, n - k0);
-    winv += (size_t)blockIdx.x * NB * NB;
+    winv += (size_t)blk * NB * NB;
   }
   double* Ab = A + (size_t)k0 + (size_t)k0 * lda;
   STAMP(0);
@@ -368,6 +366,189 @@ __global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __r
     atomicAdd(&g_diag_stamps[9], 1ull);
   }
 #endif
+}
+
+template <int NB>
+__global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __restrict__ A,
+                                                                  size_t lda, int n, int kglob,
+                                                                  int* __restrict__ info,
+                                                                  double* __restrict__ winv,
+                                                                  int mode) {
+  diag_block_body<NB>(A, lda, n, kglob, info, winv, mode, blockIdx.x);
+}
+
+// ---- square-panel factorisation: one launch per outer panel ------------------------------
+// Factors the kw x kw diagonal square of the outer row panel in place (U upper, lower
+// untouched), writes each 128-block's inverse to its winv slot, and forms the square's
+// inverse U_sq^{-1} (kw x kw, ld kw, only blocks on/above the diagonal) so the rest of the
+// row panel is ONE GEMM (X = U_sq^{-T} A_rest).  Before this, the panel took 8 diag launches
+// and 16 GEMM launches per outer step, each waiting ~0.3 ms for a CU slot beside the
+// trailing SYRK (trace r01).
+//
+// Workgroup c (ticket order) owns column tile c (128 columns) of the square.  Step j:
+// workgroup j factors block (j, j) (diag_block_body) and publishes; workgroup c > j forms
+// U(j, c) = W_j^T A(j, c) in place, publishes, then updates A(i, c) -= U(j, i)^T U(j, c) for
+// j < i <= c (U(j, i) from workgroup i).  prog[c] counts the final strips of tile c.  Data
+// crosses workgroups only after its final write and through agent-scope release/acquire
+// (MI355X guide, inter-workgroup visibility); no workgroup reads another's block before the
+// flag that publishes it, so no XCD can hold a stale copy of it.  Inverse, block column c
+// (workgroup c): X_cc = W_c, X_ic = -W_i sum_{t=i+1..c} U(i, t) X_tc for i = c-1 .. 0.
+
+// acc[bi][bj][r] += sum_t P[m*pm + t*pt] Q[t*qt + n*qn] for the wave's 64x64 share of a
+// 128x128 tile: m = 64 (w & 1) + 16 bi + (lane >> 4) + 4 r... (A-operand rows), n = 64 (w >> 1)
+// + 16 bj + (lane & 15).  Operands come straight from L2 (small, hot blocks).
+__device__ __forceinline__ void sq_mma(d4v (&acc)[4][4], const double* __restrict__ P,
+                                       size_t pm, size_t pt, const double* __restrict__ Q,
+                                       size_t qt, size_t qn, int K, int mv, int nv) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int mb = 64 * (w & 1), nbase = 64 * (w >> 1);
+#pragma unroll 8
+  for (int t0 = 0; t0 < K; t0 += 4) {
+    const int t = t0 + (lane >> 4);
+    double a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mb + 16 * i + (lane & 15);
+      a[i] = (t < K && m < mv) ? P[(size_t)m * pm + (size_t)t * pt] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nn = nbase + 16 * j + (lane & 15);
+      b[j] = (t < K && nn < nv) ? Q[(size_t)t * qt + (size_t)nn * qn] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void sq_zero(d4v (&acc)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = d4v{0.0, 0.0, 0.0, 0.0};
+}
+
+// C[m*cm + n*cn] = alpha acc + beta C for m < mv, n < nv (and m <= n when upper)
+__device__ __forceinline__ void sq_store(const d4v (&acc)[4][4], double* C, size_t cm, size_t cn,
+                                         double alpha, double beta, int mv, int nv, bool upper) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int mb = 64 * (w & 1), nbase = 64 * (w >> 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mb + 16 * i + (lane >> 4) + 4 * r, nn = nbase + 16 * j + (lane & 15);
+        if (m < mv && nn < nv && (!upper || m <= nn)) {
+          double* p = C + (size_t)m * cm + (size_t)nn * cn;
+          *p = beta != 0.0 ? fma(beta, *p, alpha * acc[i][j][r]) : alpha * acc[i][j][r];
+        }
+      }
+}
+
+// publish prog[c] = v after this workgroup's stores (guide: vmcnt drain, barrier, agent
+// release, relaxed flag store)
+__device__ __forceinline__ void sq_publish(int* prog, int c, int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&prog[c], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// wait until prog[c] >= v (one lane polls; agent acquire; barrier).  Bounded: after ~4 s
+// of polling the factorisation is flagged (info = -1) and the wait gives up, so the grid
+// always drains.
+__device__ __forceinline__ void sq_wait(int* prog, int c, int v, int* info) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    long long spins = 0;
+    while (__hip_atomic_load(&prog[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins > (1ll << 24)) {
+        ok = 0;
+        break;
+      }
+    }
+    if (!ok) atomicCAS(info, 0, -1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_ok = ok;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256, 1) void square_panel_kernel(double* __restrict__ A, size_t lda,
+                                                              int n, int k, int kw,
+                                                              double* __restrict__ winv,
+                                                              double* __restrict__ sqinv,
+                                                              int* __restrict__ info,
+                                                              int* __restrict__ sync) {
+  constexpr int NB = 128;
+  __shared__ int s_tile;
+  // latency-bound chain beside the MFMA-saturating trailing update: take issue priority
+  __builtin_amdgcn_s_setprio(3);
+  if (threadIdx.x == 0) s_tile = atomicAdd(&sync[0], 1);
+  __syncthreads();
+  const int c = s_tile;
+  int* prog = sync + 1;
+  auto blk = [&](int i, int j) { return A + (size_t)(k + i * NB) + (size_t)(k + j * NB) * lda; };
+  auto wid = [&](int i) { return min(NB, kw - i * NB); };
+  auto W = [&](int i) { return winv + (size_t)((k / NB) + i) * NB * NB; };
+  const int cw = wid(c);
+  d4v acc[4][4];
+  for (int j = 0; j < c; ++j) {
+    const int jw = wid(j);
+    sq_wait(prog, j, j + 1, info);                       // U_jj, W_j final
+    sq_zero(acc);                                        // U(j, c) = W_j^T A(j, c)
+    sq_mma(acc, W(j), NB, 1, blk(j, c), 1, lda, jw, jw, cw);
+    __syncthreads();                                     // in place: all reads first
+    sq_store(acc, blk(j, c), 1, lda, 1.0, 0.0, jw, cw, false);
+    sq_publish(prog, c, j + 1);
+    for (int i = j + 1; i <= c; ++i) {                   // A(i, c) -= U(j, i)^T U(j, c)
+      if (i < c) sq_wait(prog, i, j + 1, info);
+      sq_zero(acc);
+      sq_mma(acc, blk(j, i), lda, 1, blk(j, c), 1, lda, jw, wid(i), cw);
+      sq_store(acc, blk(i, c), 1, lda, -1.0, 1.0, wid(i), cw, i == c);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // step c: factor the diagonal block (own tile, updated by this workgroup only)
+  diag_block_body<NB>(A, lda, n, k + c * NB, info, W(c), 1, 0);
+  sq_publish(prog, c, c + 1);
+  // inverse, block column c
+  double* X = sqinv + (size_t)(c * NB) * kw;             // column block c of U_sq^{-1}
+  for (int e = threadIdx.x; e < NB * NB; e += 256) {
+    const int r = e % NB, q = e / NB;
+    if (r < cw && q < cw) X[(size_t)(c * NB + r) + (size_t)q * kw] = W(c)[r + (size_t)q * NB];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int i = c - 1; i >= 0; --i) {
+    const int iw = wid(i);
+    sq_zero(acc);                                        // S = sum_t U(i, t) X_tc
+    for (int t = i + 1; t <= c; ++t) {
+      if (t < c) sq_wait(prog, t, i + 1, info);
+      sq_mma(acc, blk(i, t), 1, lda, X + t * NB, 1, kw, wid(t), iw, cw);
+    }
+    sq_store(acc, X + i * NB, 1, kw, 1.0, 0.0, iw, cw, false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    sq_zero(acc);                                        // X_ic = -W_i S
+    sq_mma(acc, W(i), 1, NB, X + i * NB, 1, kw, iw, iw, cw);
+    __syncthreads();
+    sq_store(acc, X + i * NB, 1, kw, -1.0, 0.0, iw, cw, false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 }
 
 // ---- small-RHS triangular solves (TRSV-like, nrhs <= 16 per launch) --------------------
@@ -745,6 +926,41 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   return 0;
 }
 
+// Outer panel rows [k, k+kw) by the square kernel + one GEMM (see square_panel_kernel).
+// U_sq^{-1} of panel k / nb2 is kept in ctx->dsqinv for the solves.
+int factor_panel_sq(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  constexpr int NB = 128;
+  const int nb2 = std::max(NB, (ctx->nb2 / NB) * NB);   // as potrf_core
+  const int nsq = (kw + NB - 1) / NB;
+  const size_t slots = (size_t)((n + nb2 - 1) / nb2);
+  GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap, slots * nb2 * nb2));
+  if (!ctx->dsync) HIP_TRY(ctx, hipMalloc((void**)&ctx->dsync, 4096));
+  double* sq = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2;
+  HIP_TRY(ctx, hipMemsetAsync(ctx->dsync, 0, sizeof(int) * (nsq + 1), ctx->ls));
+  {
+    TimerScope ts(ctx, TC_PANEL, 0.0);
+    square_panel_kernel<<<nsq, 256, 0, ctx->ls>>>(A, (size_t)lda, n, k, kw, ctx->winv, sq,
+                                                   ctx->dinfo, ctx->dsync);
+    LAUNCH_CHECK(ctx);
+  }
+  const int nrest = n - k - kw;
+  if (nrest <= 0) return 0;
+  GPR_TRY(ensure_buf(ctx, &ctx->dpanel, &ctx->panel_cap, (size_t)kw * nrest));
+  GemmArgs g{};
+  g.P = sq; g.ldp = kw;                                  // U_sq^{-1}, upper triangular
+  g.Q = A + k + (size_t)(k + kw) * lda; g.ldq = lda;     // rows [k, k+kw) right of the square
+  g.C = ctx->dpanel; g.ldc = kw;                         // out of place: tiles share Q columns
+  g.M = kw; g.N = nrest; g.K = kw;
+  g.alpha = 1.0; g.beta = 0.0;
+  g.kend_from_m = 1;
+  g.info = ctx->dinfo;
+  GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
+  HIP_TRY(ctx, hipMemcpy2DAsync(A + k + (size_t)(k + kw) * lda, sizeof(double) * lda, ctx->dpanel,
+                                sizeof(double) * kw, sizeof(double) * kw, nrest,
+                                hipMemcpyDeviceToDevice, ctx->ls));
+  return 0;
+}
+
 // TRSM panel: X_j = W_j^T B_j for the inner blocks of rows [k, k+kw), each followed by
 // the update of the remaining rows of the outer block (K = nb).
 int trsm_panel(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int ncols, int ldb,
@@ -795,7 +1011,12 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
   HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
   if (s0 != user) HIP_TRY(ctx, hipStreamWaitEvent(s0, e0, 0));
   ctx->ls = s1;
-  int rc = factor_panel(ctx, dA, n, lda, 0, std::min(nb2, n));
+  const bool sqp = ctx->panel_sq && nb == 128 && nb2 <= 2048;
+  auto panel = [&](int k, int kw) {
+    return sqp ? factor_panel_sq(ctx, dA, n, lda, k, kw) : factor_panel(ctx, dA, n, lda, k, kw);
+  };
+  ctx->sqinv_nb2 = 0;
+  int rc = panel(0, std::min(nb2, n));
   hipEvent_t ev_p = sync_event(ctx, ev++);
   hipEvent_t ev_b = nullptr;
   if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
@@ -813,7 +1034,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
     a.mask_upper = 1;
     a.info = ctx->dinfo;
     if ((rc = launch_gemm_tn(ctx, a, TC_PANEL))) break;
-    if ((rc = factor_panel(ctx, dA, n, lda, kend, w2))) break;
+    if ((rc = panel(kend, w2))) break;
     hipEvent_t ev_p_next = sync_event(ctx, ev++);
     if (hipEventRecord(ev_p_next, s1) != hipSuccess) { rc = GPR_E_HIP; break; }
     // ---- main stream: b_s
@@ -864,6 +1085,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
   HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, user));
   HIP_TRY(ctx, hipStreamSynchronize(user));
   if (info) *info = hinfo;
+  if (hinfo == 0 && sqp) ctx->sqinv_nb2 = nb2;
   if (hinfo == 0) {
     ctx->fac_valid = true;
     ctx->fac_ptr = dA;

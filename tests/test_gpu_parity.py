@@ -167,6 +167,43 @@ def test_potrf_upper(n, nb):
     assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
 
 
+@pytest.mark.parametrize("panel_sq", ["1", "0"])
+@pytest.mark.parametrize("n,nb2", [(300, 256), (1000, 256), (1300, 512), (2600, 1024), (1024, 1024),
+                                   (1025, 1024), (777, 2048)])
+def test_potrf_outer_panels(n, nb2, panel_sq, monkeypatch):
+    """Two-level factorisation across outer-panel boundaries (square-panel kernel + rest
+    GEMM, and the per-block path), ragged last panels and tiles."""
+    monkeypatch.setenv("GPR_PANEL_SQ", panel_sq)
+    ctx = G.Context(0)
+    assert G._lib.lib.gpr_set_outer_block(ctx.h, nb2) == 0
+    A = _spd(n, seed=n + nb2)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    R = ctx.host(dA)
+    U = sla.cholesky(A, lower=False)
+    assert relnorm(np.triu(R), U) < 1e-12
+    assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
+    # the factor's block inverses / square inverses feed the solves
+    B = np.random.default_rng(3).random((n, 3))
+    dB = ctx.colmajor(B)
+    assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                      ctypes.c_void_p(dB.data_ptr()), 3, n) == 0
+    assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
+
+
+@pytest.mark.parametrize("panel_sq", ["1", "0"])
+@pytest.mark.parametrize("j", [0, 255, 256, 700, 1299])
+def test_potrf_not_posdef_info_later_panels(j, panel_sq, monkeypatch):
+    monkeypatch.setenv("GPR_PANEL_SQ", panel_sq)
+    ctx = G.Context(0)
+    assert G._lib.lib.gpr_set_outer_block(ctx.h, 256) == 0
+    A = _spd(1300, seed=2)
+    A[j, j] = -1.0
+    _, info = _dev_potrf(ctx, A)
+    _, info_ref = sla.lapack.dpotrf(A, lower=0)
+    assert info == info_ref == j + 1
+
+
 @pytest.mark.parametrize("j", [0, 5, 127, 128, 200])
 def test_potrf_not_posdef_info(j):
     """Non-PD input: info = order of the failing leading minor (dpotrf / PosDefException)."""

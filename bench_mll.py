@@ -1,0 +1,138 @@
+"""C4 benchmark: negative log-marginal-likelihood + its gradient (BASELINE config 4).
+
+  python bench_mll.py [--steps K --warmup W]          # 1 GPU (replicas: --gpus N via
+                                                      #  torch.distributed.run, no collective)
+
+Workload (synthetic, seeded): SE+WN kernel (D = d + 2 hyper-parameters), N = 16384,
+d = 16, y = sin(sum x)^2.  One step = what loss_grad!(MLL, F, G, hp, md, tc) does for an
+MllGradCache (src/cost.jl:50-58, 83-111, 113-126): K assembly, POTRF, alpha = K^{-1} y,
+K^{-1} (POTRI), the MLL value and all D gradient components with the log-scale chain rule
+(src/cost.jl:60-70).  Stage times come from HIP events on the context stream.
+Algorithmic work: POTRF N^3/3, POTRI 2N^3/3 (reference-style ldiv!(kchol, I) = 2N^3),
+gradient pass 8N^2 bytes (K^{-1} read once; dK recomputed per tile, never stored).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gaussianprocessregression.jl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP64_PEAK = 78.6
+HBM_PEAK = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--d", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import gpr_amd as G
+    from gpr_amd import _lib
+
+    lib = _lib.lib
+    ctx = G.Context(local)
+    N, d = a.n, a.d
+    kinds = [1, 2]
+    hp = np.r_[1.0, [3.0 * math.sqrt(8.0 / d)] * d, 0.1]
+    D = len(hp)
+    karr = (ctypes.c_int * 2)(*kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    x = np.random.default_rng(0 + rank).random((d, N))
+    y = np.sin(x.sum(0)) ** 2
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, Kinv, alpha = ctx.empty(N, N), ctx.empty(N, N), ctx.empty(N)
+    g = np.zeros(D)
+    gp = g.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    mllv = ctypes.c_double(0.0)
+    info = ctypes.c_int(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+
+    def step(events=None):
+        rec = (lambda i: events[i].record(ctx.stream)) if events else (lambda i: None)
+        rec(0)
+        ctx.check(lib.gpr_kernel(ctx.h, karr, 2, hpp, d, P(dx), N, None, N, 1, 1e-8, P(K), N), "kernel")
+        rec(1)
+        ctx.check(lib.gpr_potrf_upper(ctx.h, P(K), N, N, ctypes.byref(info)), "potrf")
+        if info.value != 0:
+            raise RuntimeError(f"not PD: info={info.value}")
+        rec(2)
+        alpha.copy_(dy)
+        ctx.check(lib.gpr_potrs_upper(ctx.h, P(K), N, N, P(alpha), 1, N), "potrs")
+        rec(3)
+        ctx.check(lib.gpr_potri_upper(ctx.h, P(K), N, N, P(Kinv), N), "potri")
+        rec(4)
+        ctx.check(lib.gpr_mll(ctx.h, P(K), N, N, P(dy), P(alpha), ctypes.byref(mllv)), "mll")
+        ctx.check(lib.gpr_mll_grad(ctx.h, karr, 2, hpp, d, P(dx), N, P(Kinv), N, P(alpha), 1e-8, 1, gp),
+                  "mll_grad")
+        rec(5)
+
+    with torch.cuda.stream(ctx.stream):
+        for _ in range(a.warmup):
+            step()
+        ctx.sync()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        ctx.sync()
+        if world > 1:
+            dist.barrier()
+        dt = (time.perf_counter() - t0) / a.steps
+        e = [ev() for _ in range(6)]
+        step(e)
+        ctx.sync()
+    names = ["kbuild", "potrf", "potrs", "potri", "mll+grad"]
+    st = {nm: e[i].elapsed_time(e[i + 1]) for i, nm in enumerate(names)}
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank == 0:
+        potrf_tf = N ** 3 / 3 / (st["potrf"] * 1e-3) / 1e12
+        potri_tf = 2 * N ** 3 / 3 / (st["potri"] * 1e-3) / 1e12
+        grad_gbs = 8.0 * N * N / (st["mll+grad"] * 1e-3) / 1e9
+        print(json.dumps({
+            "metric": "MLL + gradient evaluations/s (C4)",
+            "value": world / dt,
+            "unit": "loss_grad! evaluations/s (N=%d, d=%d, D=%d, per GPU)" % (N, d, D),
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (x ~ U[0,1)^(d x N) seeded, y = sin(sum x)^2)",
+            "config": {"workload": f"C4 MLL+grad SE+WN N={N} d={d}", "parallelism": f"replicas x{world}"},
+            "stage_ms": st,
+            "potrf_TFLOPs": potrf_tf, "potri_TFLOPs_2n3_3": potri_tf,
+            "grad_pass_GBps_Kinv_read": grad_gbs, "grad_pass_hbm_frac": grad_gbs / HBM_PEAK,
+            "mll": mllv.value, "grad_finite": bool(np.isfinite(g).all()),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -78,6 +78,8 @@ struct gpr_ctx {
   double* dsqinv = nullptr;     // U_sq^{-1} of every outer panel square (nb2^2 per slot)
   size_t sqinv_cap = 0;         // doubles
   int sqinv_nb2 = 0;            // nb2 the slots were written with (0 = none valid)
+  const double* sq_ptr = nullptr;  // factor the slots belong to
+  int sq_n = 0, sq_ld = 0;
   double* dpanel = nullptr;     // out-of-place result of the panel's rest GEMM
   size_t panel_cap = 0;
   double* dtrsv = nullptr;      // single-launch triangular sweep hand-off vector (n x 2)

@@ -455,7 +455,10 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   a.tiles_n = (g.N + TN - 1) / TN;
   static const int genv = getenv("GPR_GEMM_GROUP") ? atoi(getenv("GPR_GEMM_GROUP")) : 8;
   static const int xenv = getenv("GPR_GEMM_XCD") ? atoi(getenv("GPR_GEMM_XCD")) : 1;
-  a.xcd_remap = xenv;
+  // the XCD remap hands each XCD a contiguous range of tiles (L2 locality); with per-tile
+  // K ranges (kfrom_n / kend_from_m) that range would hold all the heavy tiles of one end
+  // of the triangle, so those launches keep the round-robin dispatch order (balanced XCDs)
+  a.xcd_remap = xenv && !g.kfrom_n && !g.kend_from_m;
   static const int dbg = getenv("GPR_GEMM_DBG_L2") ? 1 : 0;
   a.dbg = dbg;
   a.gm = std::max(1, std::min(genv, a.tiles_m));

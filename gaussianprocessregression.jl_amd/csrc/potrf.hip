@@ -424,6 +424,80 @@ __device__ __forceinline__ void sq_mma(d4v (&acc)[4][4], const double* __restric
   }
 }
 
+// LDS-staged form of sq_mma (16-deep K chunks, register-prefetched, double-buffered).
+// PM: P is m-contiguous (element (m, t) at P[m + t*pld]); else t-contiguous (P[t + m*pld]).
+// Q element (t, n) at Q[t + n*qld].  lds: 2 buffers x (P image 128x16 + Q image 128x16).
+// Images use the GEMM kernel's swizzled [row][16] layout (conflict-free ds_read_b128).
+constexpr int SQ_KC = 16;
+__device__ __forceinline__ int sq_idx(int row, int chunk) {
+  return row * SQ_KC + ((chunk ^ ((row >> 1) & 7)) << 1);
+}
+template <bool PM>
+__device__ __forceinline__ void sq_gemm(d4v (&acc)[4][4], const double* __restrict__ P, size_t pld,
+                                        const double* __restrict__ Q, size_t qld, int K, int mv,
+                                        int nv, double* lds) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int mb = 64 * (w & 1), nbase = 64 * (w >> 1);
+  const int nch = (K + SQ_KC - 1) / SQ_KC;
+  double rp[8], rq[8];
+  auto gload = [&](int c) {
+    const int t0 = c * SQ_KC;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 256 * r;
+      int m, t;
+      if (PM) { m = e & 127; t = e >> 7; } else { m = e >> 4; t = e & 15; }
+      const bool ok = m < mv && t0 + t < K;
+      rp[r] = ok ? (PM ? P[(size_t)m + (size_t)(t0 + t) * pld] : P[(size_t)(t0 + t) + (size_t)m * pld]) : 0.0;
+      const int nn = e >> 4, tq = e & 15;
+      rq[r] = (nn < nv && t0 + tq < K) ? Q[(size_t)(t0 + tq) + (size_t)nn * qld] : 0.0;
+    }
+  };
+  auto lstore = [&](int buf) {
+    double* pi = lds + buf * 4096;
+    double* qi = pi + 2048;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + 256 * r;
+      int m, t;
+      if (PM) { m = e & 127; t = e >> 7; } else { m = e >> 4; t = e & 15; }
+      pi[sq_idx(m, t >> 1) + (t & 1)] = rp[r];
+      const int nn = e >> 4, tq = e & 15;
+      qi[sq_idx(nn, tq >> 1) + (tq & 1)] = rq[r];
+    }
+  };
+  __syncthreads();  // LDS free (previous users done)
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) gload(c + 1);
+    const double* pi = lds + (c & 1) * 4096;
+    const double* qi = pi + 2048;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int ch = (lane >> 4) + 4 * p;
+      d2 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const d2*>(&pi[sq_idx(mb + 16 * i + (lane & 15), ch)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *reinterpret_cast<const d2*>(&qi[sq_idx(nbase + 16 * j + (lane & 15), ch)]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][h], b[j][h], acc[i][j], 0, 0, 0);
+    }
+    if (c + 1 < nch) lstore((c + 1) & 1);
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ void sq_zero(d4v (&acc)[4][4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -493,6 +567,7 @@ __global__ __launch_bounds__(256, 1) void square_panel_kernel(double* __restrict
                                                               int* __restrict__ sync) {
   constexpr int NB = 128;
   __shared__ int s_tile;
+  __shared__ double glds[2 * 4096];  // tile-product staging (64 KB)
   // latency-bound chain beside the MFMA-saturating trailing update: take issue priority
   __builtin_amdgcn_s_setprio(3);
   if (threadIdx.x == 0) s_tile = atomicAdd(&sync[0], 1);
@@ -508,14 +583,14 @@ __global__ __launch_bounds__(256, 1) void square_panel_kernel(double* __restrict
     const int jw = wid(j);
     sq_wait(prog, j, j + 1, info);                       // U_jj, W_j final
     sq_zero(acc);                                        // U(j, c) = W_j^T A(j, c)
-    sq_mma(acc, W(j), NB, 1, blk(j, c), 1, lda, jw, jw, cw);
+    sq_gemm<false>(acc, W(j), NB, blk(j, c), lda, jw, jw, cw, glds);
     __syncthreads();                                     // in place: all reads first
     sq_store(acc, blk(j, c), 1, lda, 1.0, 0.0, jw, cw, false);
     sq_publish(prog, c, j + 1);
     for (int i = j + 1; i <= c; ++i) {                   // A(i, c) -= U(j, i)^T U(j, c)
       if (i < c) sq_wait(prog, i, j + 1, info);
       sq_zero(acc);
-      sq_mma(acc, blk(j, i), lda, 1, blk(j, c), 1, lda, jw, wid(i), cw);
+      sq_gemm<false>(acc, blk(j, i), lda, blk(j, c), lda, jw, wid(i), cw, glds);
       sq_store(acc, blk(i, c), 1, lda, -1.0, 1.0, wid(i), cw, i == c);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -537,13 +612,13 @@ __global__ __launch_bounds__(256, 1) void square_panel_kernel(double* __restrict
     sq_zero(acc);                                        // S = sum_t U(i, t) X_tc
     for (int t = i + 1; t <= c; ++t) {
       if (t < c) sq_wait(prog, t, i + 1, info);
-      sq_mma(acc, blk(i, t), 1, lda, X + t * NB, 1, kw, wid(t), iw, cw);
+      sq_gemm<true>(acc, blk(i, t), lda, X + t * NB, kw, wid(t), iw, cw, glds);
     }
     sq_store(acc, X + i * NB, 1, kw, 1.0, 0.0, iw, cw, false);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     sq_zero(acc);                                        // X_ic = -W_i S
-    sq_mma(acc, W(i), 1, NB, X + i * NB, 1, kw, iw, iw, cw);
+    sq_gemm<true>(acc, W(i), NB, X + i * NB, kw, iw, iw, cw, glds);
     __syncthreads();
     sq_store(acc, X + i * NB, 1, kw, -1.0, 0.0, iw, cw, false);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -926,6 +1001,67 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   return 0;
 }
 
+// All outer-panel square inverses U_sq^{-1} of a finished factor in one launch: grid
+// (panel p, block column c).  Block column c of panel p needs only U (final) and the block
+// inverses W_i (final), so the workgroups are independent (no hand-offs).
+//   X_cc = W_c,  X_ic = -W_i sum_{t=i+1..c} U(i, t) X_tc   (i = c-1 .. 0)
+__global__ __launch_bounds__(256, 1) void sqinv_kernel(const double* __restrict__ U, size_t ldu,
+                                                       int n, int nb2,
+                                                       const double* __restrict__ winv,
+                                                       double* __restrict__ sqinv) {
+  constexpr int NB = 128;
+  __shared__ double glds[2 * 4096];
+  const int p = blockIdx.x, c = blockIdx.y;
+  const int k = p * nb2, kw = min(nb2, n - k);
+  if (c * NB >= kw) return;
+  auto blk = [&](int i, int j) { return U + (size_t)(k + i * NB) + (size_t)(k + j * NB) * ldu; };
+  auto wid = [&](int i) { return min(NB, kw - i * NB); };
+  auto W = [&](int i) { return winv + (size_t)((k / NB) + i) * NB * NB; };
+  const int cw = wid(c);
+  double* X = sqinv + (size_t)p * nb2 * nb2 + (size_t)(c * NB) * kw;
+  for (int e = threadIdx.x; e < NB * NB; e += 256) {
+    const int r = e % NB, q = e / NB;
+    if (r < cw && q < cw) X[(size_t)(c * NB + r) + (size_t)q * kw] = W(c)[r + (size_t)q * NB];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  d4v acc[4][4];
+  for (int i = c - 1; i >= 0; --i) {
+    const int iw = wid(i);
+    sq_zero(acc);
+    for (int t = i + 1; t <= c; ++t) sq_gemm<true>(acc, blk(i, t), ldu, X + t * NB, kw, wid(t), iw, cw, glds);
+    sq_store(acc, X + i * NB, 1, kw, 1.0, 0.0, iw, cw, false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    sq_zero(acc);
+    sq_gemm<true>(acc, W(i), NB, X + i * NB, kw, iw, iw, cw, glds);
+    __syncthreads();
+    sq_store(acc, X + i * NB, 1, kw, -1.0, 0.0, iw, cw, false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
+// norm[j] -= sum_{i<n} B[i + j ldb]^2 for j < ncols: one wave per column (deterministic)
+__global__ __launch_bounds__(256) void colnorm_sub_kernel(const double* __restrict__ B, size_t ldb,
+                                                          int n, int ncols, double* __restrict__ norm) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= ncols) return;
+  const double* col = B + (size_t)j * ldb;
+  double s0 = 0.0, s1 = 0.0;
+  int i = lane;
+  for (; i + 64 < n; i += 128) {
+    s0 = fma(col[i], col[i], s0);
+    s1 = fma(col[i + 64], col[i + 64], s1);
+  }
+  if (i < n) s0 = fma(col[i], col[i], s0);
+  double s = s0 + s1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) norm[j] -= s;
+}
+
 // Outer panel rows [k, k+kw) by the square kernel + one GEMM (see square_panel_kernel).
 // U_sq^{-1} of panel k / nb2 is kept in ctx->dsqinv for the solves.
 int factor_panel_sq(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
@@ -1085,7 +1221,12 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
   HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, user));
   HIP_TRY(ctx, hipStreamSynchronize(user));
   if (info) *info = hinfo;
-  if (hinfo == 0 && sqp) ctx->sqinv_nb2 = nb2;
+  if (hinfo == 0 && sqp) {
+    ctx->sqinv_nb2 = nb2;
+    ctx->sq_ptr = dA;
+    ctx->sq_n = n;
+    ctx->sq_ld = lda;
+  }
   if (hinfo == 0) {
     ctx->fac_valid = true;
     ctx->fac_ptr = dA;
@@ -1113,12 +1254,116 @@ int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
   return 0;
 }
 
+// U_sq^{-1} of every outer panel of the factor dU (computed once per factor, reused by all
+// solves).  Returns 1 when the square path is usable (nb = 128, nb2 <= 2048).
+int ensure_sq_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
+  constexpr int NB = 128;
+  const int nb2 = std::max(NB, (ctx->nb2 / NB) * NB);
+  if (ctx->nb != NB || nb2 > 2048 || getenv("GPR_TRSM_LEGACY")) return 0;
+  GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
+  if (ctx->sqinv_nb2 == nb2 && ctx->sq_ptr == dU && ctx->sq_n == n && ctx->sq_ld == ldu) return 1;
+  const int np = (n + nb2 - 1) / nb2;
+  GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap, (size_t)np * nb2 * nb2));
+  {
+    TimerScope ts(ctx, TC_OTHER, 0.0);
+    sqinv_kernel<<<dim3(np, nb2 / NB), 256, 0, ctx->stream>>>(dU, (size_t)ldu, n, nb2, ctx->winv,
+                                                              ctx->dsqinv);
+    LAUNCH_CHECK(ctx);
+  }
+  ctx->sqinv_nb2 = nb2;
+  ctx->sq_ptr = dU;
+  ctx->sq_n = n;
+  ctx->sq_ld = ldu;
+  return 1;
+}
+
 // B <- U^{-T} B (U^T X = B), GEMM-based (any nrhs), two-level with the same lookahead
 // structure as potrf_core.  norm_out: optional norm_out[c] -= ||X[:, c]||^2 (fused in the
 // panel GEMM epilogue).  lower_rhs: B is lower-triangular (identity RHS) -> outer block s
 // only touches columns [0, (s+1) nb2).
+// trsm_ut_core on the square inverses: the panel solve of outer block s is ONE GEMM,
+// X_s = U_sq_s^{-T} B_s (K range cut at each tile's diagonal, out of place + strided copy
+// back), instead of nb2/nb dependent (GEMM, update) pairs.  Same two-stream lookahead.
+// norm_out is a deterministic post-pass over the solved B.
+static int trsm_ut_sq(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
+                      int ldb, double* norm_out, int lower_rhs) {
+  const int nb2 = ctx->sqinv_nb2;
+  hipStream_t s0 = ctx->stream, s1 = ctx->stream2;
+  auto cols = [&](int kend) { return lower_rhs ? std::min(nrhs, kend) : nrhs; };
+  GPR_TRY(ensure_buf(ctx, &ctx->dpanel, &ctx->panel_cap, (size_t)nb2 * nrhs));
+  auto panel_solve = [&](int k, int kw, int nc) -> int {
+    GemmArgs g{};
+    g.P = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2; g.ldp = kw;
+    g.Q = dB + k; g.ldq = ldb;
+    g.C = ctx->dpanel; g.ldc = kw;
+    g.M = kw; g.N = nc; g.K = kw;
+    g.alpha = 1.0; g.beta = 0.0;
+    g.kend_from_m = 1;
+    GPR_TRY(launch_gemm_tn(ctx, g, TC_TRSM_GEMM));
+    HIP_TRY(ctx, hipMemcpy2DAsync(dB + k, sizeof(double) * ldb, ctx->dpanel, sizeof(double) * kw,
+                                  sizeof(double) * kw, nc, hipMemcpyDeviceToDevice, ctx->ls));
+    return 0;
+  };
+  size_t ev = 0;
+  hipEvent_t e0 = sync_event(ctx, ev++);
+  HIP_TRY(ctx, hipEventRecord(e0, s0));
+  HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
+  ctx->ls = s1;
+  const int w0 = std::min(nb2, n);
+  int rc = panel_solve(0, w0, cols(w0));
+  hipEvent_t ev_p = sync_event(ctx, ev++);
+  hipEvent_t ev_b = nullptr;
+  if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
+  for (int k = 0; !rc && k + nb2 < n; k += nb2) {
+    const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
+    const int nc = cols(kend);
+    ctx->ls = s1;
+    if (ev_b && hipStreamWaitEvent(s1, ev_b, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    GemmArgs a{};
+    a.P = dU + k + (size_t)kend * ldu; a.ldp = ldu;
+    a.Q = dB + k; a.ldq = ldb;
+    a.C = dB + kend; a.ldc = ldb;
+    a.M = w2; a.N = nc; a.K = nb2;
+    a.alpha = -1.0; a.beta = 1.0;
+    if ((rc = launch_gemm_tn(ctx, a, TC_TRSM_GEMM))) break;
+    if ((rc = panel_solve(kend, w2, cols(rest0)))) break;
+    hipEvent_t ev_p_next = sync_event(ctx, ev++);
+    if (hipEventRecord(ev_p_next, s1) != hipSuccess) { rc = GPR_E_HIP; break; }
+    ctx->ls = s0;
+    if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    if (rest0 < n) {
+      GemmArgs b{};
+      b.P = dU + k + (size_t)rest0 * ldu; b.ldp = ldu;
+      b.Q = dB + k; b.ldq = ldb;
+      b.C = dB + rest0; b.ldc = ldb;
+      b.M = n - rest0; b.N = nc; b.K = nb2;
+      b.alpha = -1.0; b.beta = 1.0;
+      if ((rc = launch_gemm_tn(ctx, b, TC_TRSM_GEMM))) break;
+    }
+    ev_b = sync_event(ctx, ev++);
+    if (hipEventRecord(ev_b, s0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    ev_p = ev_p_next;
+  }
+  ctx->ls = s0;
+  hipEvent_t ej = sync_event(ctx, ev++);
+  HIP_TRY(ctx, hipEventRecord(ej, s1));
+  HIP_TRY(ctx, hipStreamWaitEvent(s0, ej, 0));
+  if (rc) return rc;
+  if (norm_out) {
+    TimerScope ts(ctx, TC_OTHER, 0.0);
+    colnorm_sub_kernel<<<(nrhs + 3) / 4, 256, 0, s0>>>(dB, (size_t)ldb, n, nrhs, norm_out);
+    LAUNCH_CHECK(ctx);
+  }
+  return 0;
+}
+
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs) {
+  {
+    const int sqok = ensure_sq_inverses(ctx, dU, n, ldu);
+    if (sqok < 0) return sqok;
+    if (sqok == 1) return trsm_ut_sq(ctx, dU, n, ldu, dB, nrhs, ldb, norm_out, lower_rhs);
+  }
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   const int nb = ctx->nb;
   const int nb2 = std::max(nb, (ctx->nb2 / nb) * nb);

@@ -49,6 +49,8 @@ struct gpr_ctx {
   int nb2 = 1024;  // outer panel width = K of the big trailing updates (multiple of nb)
   hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
   hipStream_t stream2 = nullptr;  // lookahead panel stream (GEMMs of the panel chain)
+  hipStream_t stream3 = nullptr;  // inner lookahead: panel-update remainder beside the chain
+  int inner_la = 0;               // split the panel inner update (GPR_INNER_LA=1; no gain measured)
   hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
   hipStream_t smain = nullptr;    // big trailing updates: CU mask = all but the reserved CUs
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)

@@ -146,13 +146,15 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   // (diag factor + panel TRSM) must win CUs over the big trailing SYRK it overlaps
   int prio_lo = 0, prio_hi = 0;
   hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+  if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     delete ctx;
     return GPR_E_HIP;
   }
   if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
   if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
   if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);
+  if (const char* e = getenv("GPR_INNER_LA")) ctx->inner_la = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
   // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is
   // on the critical path of the lookahead chain.  GEMM streams get the complement mask.
@@ -207,6 +209,7 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto e : ctx->sync_events) hipEventDestroy(e);
   if (ctx->stream2) hipStreamDestroy(ctx->stream2);
+  if (ctx->stream3) hipStreamDestroy(ctx->stream3);
   if (ctx->sdiag) hipStreamDestroy(ctx->sdiag);
   if (ctx->smain) hipStreamDestroy(ctx->smain);
   if (ctx->winv) hipFree(ctx->winv);

@@ -958,12 +958,18 @@ hipEvent_t sync_event(gpr_ctx* ctx, size_t i) {
 // diag factor+inverse, in-place panel TRSM over all columns >= j+jb (MFMA GEMM with
 // U_jj^{-1}), then the update of the remaining rows of this outer panel (K = nb).
 int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  // Inner lookahead: after block j's row TRSM, only the NEXT strip (rows of block j+1) is
+  // updated on the chain stream; the remaining strips of the panel are updated on stream3
+  // beside diag(j+1) and TRSM(j+1).  Strip j+2 must hold that remainder update before the
+  // chain updates it at step j+1, so the chain waits for it there.
   const int nb = ctx->nb;
+  const bool la = ctx->inner_la && ctx->stream3;
+  hipStream_t home = ctx->ls, side = ctx->stream3;
+  hipEvent_t e_rest = nullptr;  // remainder update of the previous step (on side)
   for (int j = k; j < k + kw; j += nb) {
     const int jb = std::min(nb, n - j);
     double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
     if (ctx->diag_cus > 0) {  // hop to the reserved-CU stream and back
-      hipStream_t home = ctx->ls;
       hipEvent_t e1 = sync_event(ctx, ctx->ev_next++), e2 = sync_event(ctx, ctx->ev_next++);
       HIP_TRY(ctx, hipEventRecord(e1, home));
       HIP_TRY(ctx, hipStreamWaitEvent(ctx->sdiag, e1, 0));
@@ -986,18 +992,48 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
     g.alpha = 1.0; g.beta = 0.0;
     g.info = ctx->dinfo;
     GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
-    if (j + jb < k + kw) {
-      GemmArgs u{};
-      u.P = row; u.ldp = lda;
-      u.Q = row; u.ldq = lda;
-      u.C = A + (j + jb) + (size_t)(j + jb) * lda; u.ldc = lda;
-      u.M = k + kw - j - jb; u.N = n - j - jb; u.K = jb;
-      u.alpha = -1.0; u.beta = 1.0;
-      u.mask_upper = 1;
-      u.info = ctx->dinfo;
-      GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
+    const int rows = k + kw - j - jb;  // panel rows below block j
+    if (rows <= 0) continue;
+    const int r1 = la ? std::min(nb, rows) : rows;
+    if (la && rows > r1) {
+      // remainder strips [j+jb+r1, k+kw) on the side stream, after this TRSM
+      hipEvent_t ex = sync_event(ctx, ctx->ev_next++);
+      HIP_TRY(ctx, hipEventRecord(ex, home));
+      HIP_TRY(ctx, hipStreamWaitEvent(side, ex, 0));
+      if (e_rest) HIP_TRY(ctx, hipStreamWaitEvent(side, e_rest, 0));
+      GemmArgs u2{};
+      u2.P = A + j + (size_t)(j + jb + r1) * lda; u2.ldp = lda;  // X_j columns of those rows
+      u2.Q = row; u2.ldq = lda;
+      u2.C = A + (j + jb + r1) + (size_t)(j + jb) * lda; u2.ldc = lda;
+      u2.M = rows - r1; u2.N = n - j - jb; u2.K = jb;
+      u2.alpha = -1.0; u2.beta = 1.0;
+      u2.mask_upper = 1; u2.mask_off = -r1;  // global row <= global column
+      u2.info = ctx->dinfo;
+      ctx->ls = side;
+      const int rc = launch_gemm_tn(ctx, u2, TC_PANEL);
+      ctx->ls = home;
+      if (rc) return rc;
+    }
+    // the next strip on the chain; it must already hold the previous remainder update
+    if (e_rest) {
+      HIP_TRY(ctx, hipStreamWaitEvent(home, e_rest, 0));
+      e_rest = nullptr;
+    }
+    GemmArgs u{};
+    u.P = row; u.ldp = lda;
+    u.Q = row; u.ldq = lda;
+    u.C = A + (j + jb) + (size_t)(j + jb) * lda; u.ldc = lda;
+    u.M = r1; u.N = n - j - jb; u.K = jb;
+    u.alpha = -1.0; u.beta = 1.0;
+    u.mask_upper = 1;
+    u.info = ctx->dinfo;
+    GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
+    if (la && rows > r1) {
+      e_rest = sync_event(ctx, ctx->ev_next++);
+      HIP_TRY(ctx, hipEventRecord(e_rest, side));
     }
   }
+  if (e_rest) HIP_TRY(ctx, hipStreamWaitEvent(home, e_rest, 0));  // panel complete on home
   return 0;
 }
 

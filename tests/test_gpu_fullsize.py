@@ -1,0 +1,116 @@
+"""Parity at BASELINE.json's full sizes through size-independent properties.
+
+The oracle cannot factor N = 32768 in seconds, so at the bench configurations (C3:
+SE+SE+WN, N = 32768, d = 8, np = 8192; C4: SE+WN, N = 16384, d = 16) the HIP path is
+checked through identities that hold at any size (the small-size oracle parity lives in
+test_gpu_parity.py / test_golden.py):
+  * solve residual: ||K alpha - y|| <= 1e-11 (||K||_F ||alpha|| + ||y||)   (backward stable)
+  * factor backward error on sampled entries: |(U^T U)_ij - K_ij| <= 1e-12 ||U_:i|| ||U_:j||,
+    K_ij from the oracle's formula for the two points
+  * posterior mean at the training points: mu = K_f alpha = y - (sigma_n^2 + n_SE eps) alpha
+    (the cross kernel carries no jitter/noise, src/predict.jl:37; src/covariance.jl:49-58),
+    normwise 1e-9
+  * 0 <= diagonal variance <= prior (+ 1e-8 prior)
+  * MLL = 0.5 (y.alpha + 2 sum log U_ii + N log 2 pi) from the device factor (rel 1e-12);
+    LogScale gradient = gradient .* hp (src/cost.jl:60-70); one component against a central
+    finite difference (rel 1e-4).
+The matvec / norms here use torch on the device as an independent checker (not the product
+path).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gpr_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = pytest.importorskip("gpr_amd")
+
+
+def _cov(kinds):
+    parts = [G.SquaredExp() if k == "SE" else G.WhiteNoise() for k in kinds]
+    c = parts[0]
+    for p in parts[1:]:
+        c = c + p
+    return c
+
+
+def _hp(kinds, d):
+    return O.default_hp(kinds, d)
+
+
+def test_c3_fit_and_posterior_full_size():
+    N, d, NP = 32768, 8, 8192
+    kinds = ["SE", "SE", "WN"]
+    hp = _hp(kinds, d)
+    x, y, xp = O.synthetic(d, N, NP)
+    md = G.GPRModel(_cov(kinds), hp, x, y)
+    ctx = md.ctx
+    pc = G.GPRPredictCache(md)
+    G.core._update_predict_cache(G.core.pc_adapter(pc), md)
+    U, alpha = pc.Kxx, pc.wt
+    ctx.sync()
+    # solve residual with K rebuilt on the device
+    K = G.kernel(_cov(kinds), hp, x, host=False, ctx=ctx)
+    ctx.sync()
+    yd = torch.from_numpy(y).to(K.device)
+    r = torch.mv(K.t(), alpha) - yd            # K symmetric; column-major storage
+    scale = torch.linalg.norm(K) * torch.linalg.norm(alpha) + torch.linalg.norm(yd)
+    assert float(torch.linalg.norm(r) / scale) < 1e-11
+    # factor backward error on sampled entries (U^T U)_ij vs the oracle's K_ij
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(N, size=64, replace=False))
+    # tensor row c = column c of the column-major factor; only rows k <= c belong to U
+    # (the strict lower triangle still holds K, dpotrf 'U' semantics)
+    it = torch.from_numpy(idx).to(K.device)
+    Ucols = U.index_select(0, it).t().clone()                              # N x 64: U[:, idx]
+    below = torch.arange(N, device=K.device)[:, None] > it[None, :]
+    Ucols[below] = 0.0
+    UtU = (Ucols.t() @ Ucols).cpu().numpy()
+    Kij = O.kernel(kinds, hp, x[:, idx], None)
+    nrm = np.linalg.norm(Ucols.cpu().numpy(), axis=0)
+    assert np.all(np.abs(UtU - Kij) <= 1e-12 * np.outer(nrm, nrm))
+    del K
+    # posterior mean at the training points: mu = y - (sigma_n^2 + nse eps) alpha
+    sub = idx
+    mu_t = G.predict_mean(md, x[:, sub])
+    a_h = alpha.cpu().numpy()
+    expect = y[sub] - (0.1 ** 2 + 2 * O.EPS_DEFAULT) * a_h[sub]
+    assert np.linalg.norm(mu_t - expect) <= 1e-9 * np.linalg.norm(expect)
+    # diagonal variance bounds at the bench's test points
+    mu, var = G.predict(md, xp, diagonal_var=True)
+    prior = O.diag_prior(kinds, hp, d)
+    assert np.isfinite(mu).all()
+    assert var.min() >= -1e-8 * prior and var.max() <= prior * (1 + 1e-8)
+
+
+def test_c4_mll_and_gradient_full_size():
+    N, d = 16384, 16
+    kinds = ["SE", "WN"]
+    hp = _hp(kinds, d)
+    x, y, _ = O.synthetic(d, N)
+    md = G.GPRModel(_cov(kinds), hp, x, y)
+    ctx = md.ctx
+    tc = G.MllGradCache(md)
+    G.update_cache_(tc, hp, md)
+    L = G.loss(G.MarginalLikelihood(), hp, md)
+    ctx.sync()
+    a_h = tc.alpha.cpu().numpy()
+    diagU = torch.diagonal(tc.kchol_base).cpu().numpy()
+    L_ref = 0.5 * (float(y @ a_h) + 2.0 * float(np.sum(np.log(diagU))) + N * math.log(2 * math.pi))
+    assert L == pytest.approx(L_ref, rel=1e-12)
+    g = G.grad(G.MarginalLikelihood(), hp, md)
+    F = np.zeros(1)
+    Gl = np.zeros(len(hp))
+    G.log_loss_grad_(G.MarginalLikelihood(), F, Gl, np.log(hp), md, tc)
+    np.testing.assert_allclose(Gl, g * hp, rtol=1e-12, atol=0)
+    # central finite difference on the noise component and on sigma of the SE part
+    for i in (0, len(hp) - 1):
+        h = 1e-5 * hp[i]
+        hp_p, hp_m = hp.copy(), hp.copy()
+        hp_p[i] += h
+        hp_m[i] -= h
+        fd = (G.loss(G.MarginalLikelihood(), hp_p, md) - G.loss(G.MarginalLikelihood(), hp_m, md)) / (2 * h)
+        assert fd == pytest.approx(g[i], rel=1e-4)

@@ -79,14 +79,15 @@ __device__ __forceinline__ bool tile_coords(const GemmK& a, int& m0, int& n0) {
 
 // C = alpha * acc (o E) + beta * C on the tile, optional column sum-of-squares into norm_out.
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, d4 (&acc)[4][4], int m0, int n0,
-                                              double* red) {
+                                              double* red, bool preloaded = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
   // ---- epilogue: all loads first (C, E), then all stores -- interleaving them through
   // possibly-aliasing pointers would serialise one HBM round trip per element.
   double* __restrict__ Cp = g.C;
   const double* __restrict__ Ep = g.E;
-  const bool has_beta = g.beta != 0.0;
+  // preloaded: the accumulators started at (beta/alpha) C, so C is not read again here
+  const bool has_beta = g.beta != 0.0 && !preloaded;
   const bool has_e = Ep != nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -298,7 +299,7 @@ __device__ __forceinline__ int pipe_idx(int row, int chunk) {
 // TKS = 8, OCC = 2: two workgroups per CU, 16-KB stages, 32 MFMAs per stage -- a second
 //   workgroup hides each tile's prologue fill and C epilogue, which matter at short K (the
 //   K = nb2 trailing updates of POTRF and the TRSM).
-template <int TKS>
+template <int TKS, bool PRELOAD>
 __device__ __forceinline__ void gemm_tn_pipe_body(const GemmK& a) {
   constexpr int STAGE_D = (TM + TN) * TKS;      // doubles per stage (P image, then Q)
   constexpr int NCH = TKS / 2;                  // 16-B chunks per row
@@ -360,11 +361,34 @@ __device__ __forceinline__ void gemm_tn_pipe_body(const GemmK& a) {
         F[p][4 + j] = *reinterpret_cast<const d2*>(&ps[pipe_idx<TKS>(wm * 64 + j * 16 + (lane & 15), ch)]);
     }
   };
+  // PRELOAD (host picks it for beta != 0, alpha != 0, no Hadamard factor): the tile of C
+  // is read up front into the accumulators as (beta/alpha) C -- 64 independent loads per
+  // lane in one batch instead of a dependent load->store round trip in the epilogue (which
+  // bounds the short-K chain GEMMs); the epilogue then only stores alpha acc.  A compile-
+  // time switch: a runtime branch merging two accumulator initialisations miscompiles.
   d4 acc[4][4];
+  if constexpr (PRELOAD) {
+    const double sc = g.beta / g.alpha;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) mfma_agpr_zero(acc[i][j]);
+      for (int r = 0; r < 4; ++r) {
+        const int nn = n0 + wn * 64 + i * 16 + (lane >> 4) + 4 * r;
+        const double* col = g.C + (size_t)min(nn, g.N - 1) * g.ldc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // clamped address + select: branch-free, all 64 loads in flight together
+          const int mm = m0 + wm * 64 + j * 16 + (lane & 15);
+          const double c = col[min(mm, g.M - 1)];
+          acc[i][j][r] = (mm < g.M && nn < g.N) ? sc * c : 0.0;
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mfma_agpr_zero(acc[i][j]);
+  }
   auto mfma_stage = [&](const d2 (&F)[NP][8]) {
 #pragma unroll
     for (int p = 0; p < NP; ++p)
@@ -421,11 +445,13 @@ __device__ __forceinline__ void gemm_tn_pipe_body(const GemmK& a) {
   if (s < nst) mfma_stage(F0);
   wait_vmcnt<0>();
   __syncthreads();  // the epilogue's norm reduction reuses LDS
-  gemm_epilogue(g, acc, m0, n0, lds + PBUF * STAGE_D);
+  gemm_epilogue(g, acc, m0, n0, lds + PBUF * STAGE_D, PRELOAD);
 }
 
-__global__ __launch_bounds__(256, 1) void gemm_tn_pipe16_kernel(GemmK a) { gemm_tn_pipe_body<16>(a); }
-__global__ __launch_bounds__(256, 2) void gemm_tn_pipe8_kernel(GemmK a) { gemm_tn_pipe_body<8>(a); }
+__global__ __launch_bounds__(256, 1) void gemm_tn_pipe16_kernel(GemmK a) { gemm_tn_pipe_body<16, false>(a); }
+// pipe8: C preloaded (beta != 0, the SYRK / TRSM updates); pipe8z: zero-initialised
+__global__ __launch_bounds__(256, 2) void gemm_tn_pipe8_kernel(GemmK a) { gemm_tn_pipe_body<8, true>(a); }
+__global__ __launch_bounds__(256, 2) void gemm_tn_pipe8z_kernel(GemmK a) { gemm_tn_pipe_body<8, false>(a); }
 
 }  // namespace
 
@@ -500,8 +526,12 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   if (pipe && long_k)
     gemm_tn_pipe16_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
   else if (pipe) {
+    static const bool nopre = getenv("GPR_GEMM_NOPRELOAD") != nullptr;
     TimerScope tk(ctx, TC_GEMM_PIPE, flops);
-    gemm_tn_pipe8_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
+    if (g.beta != 0.0 && g.alpha != 0.0 && !g.E && !nopre)
+      gemm_tn_pipe8_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
+    else
+      gemm_tn_pipe8z_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
   }
   else if (vec)
     gemm_tn_kernel<true><<<(unsigned)nblk, 256, pad, ctx->ls>>>(a);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "../gaussianprocessregression.jl_amd/csrc/common.hpp"
 
@@ -11,6 +12,34 @@ __global__ void init_kernel(double* p, size_t n, unsigned seed) {
     unsigned h = (unsigned)(i * 2654435761u) ^ seed;
     h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
     p[i] = (h & 0xffffff) / 16777216.0 - 0.5;
+  }
+}
+
+__device__ double init_val(size_t i, unsigned seed) {
+  unsigned h = (unsigned)(i * 2654435761u) ^ seed;
+  h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
+  return (h & 0xffffff) / 16777216.0 - 0.5;
+}
+
+// max |C - (C0 - P^T P)| over a strided sample of (m, n) (upper: m <= n only, the rest
+// must still hold C0); err as the bit pattern of a non-negative double
+__global__ void verify_kernel(const double* P, const double* C, int N, int K, int upper, int stride,
+                              unsigned long long* err) {
+  const int ns = (N + stride - 1) / stride;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)ns * ns;
+       t += (size_t)gridDim.x * blockDim.x) {
+    // offsets cycle through every residue mod stride, so all tile positions are hit
+    const int m = min(N - 1, (int)(t % ns) * stride + (int)(t / ns) % stride);
+    const int n = min(N - 1, (int)(t / ns) * stride + (int)(t % ns) % stride);
+    const size_t i = (size_t)m + (size_t)n * N;
+    double ref = init_val(i, 2);
+    if (!upper || m <= n) {
+      double acc = 0.0;
+      for (int k = 0; k < K; ++k) acc += P[k + (size_t)m * K] * P[k + (size_t)n * K];
+      ref -= acc;
+    }
+    const double e = fabs(C[i] - ref);
+    atomicMax(err, (unsigned long long)__double_as_longlong(e != e ? 1e300 : e));
   }
 }
 
@@ -79,6 +108,19 @@ int main(int argc, char** argv) {
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     if (rep >= 2) printf("gemm mode=%d N=%d K=%d: %.3f ms  %.2f TFLOP/s\n", mode, N, K, ms, flops / ms / 1e9);
+  }
+  if (getenv("GEMM_VERIFY")) {
+    init_kernel<<<1024, 256, 0, s>>>(C, (size_t)N * N, 2);
+    launch_gemm_tn(ctx, g, TC_OTHER);
+    unsigned long long* derr;
+    hipMalloc(&derr, 8);
+    hipMemsetAsync(derr, 0, 8, s);
+    verify_kernel<<<2048, 256, 0, s>>>(P, C, N, K, g.upper, 7, derr);
+    unsigned long long herr = 0;
+    hipStreamSynchronize(s);
+    hipMemcpy(&herr, derr, 8, hipMemcpyDeviceToHost);
+    double e; memcpy(&e, &herr, 8);
+    printf("verify mode=%d N=%d K=%d: max abs err %.3e %s\n", mode, N, K, e, e < 1e-12 * K ? "OK" : "FAIL");
   }
   return 0;
 }

@@ -1,10 +1,8 @@
-set -o pipefail
-mkdir -p gpurun_out
-{
-timeout -k 10 400 python -m pytest tests -m gpu -q -x > gpurun_out/t4.log 2>&1; echo "pytest rc=$?"; tail -3 gpurun_out/t4.log
-for nb2 in 128 256 512 768 1024; do
-  echo "== nb2=$nb2"; GPR_NB2=$nb2 timeout -k 5 100 ./tools/gemm_bench 32768 0 2 | tail -4
+#!/bin/bash
+# POTRF N=32768 stage breakdown across outer-panel widths (GPR_NB2).
+set -e
+cd "$(dirname "$0")/.."
+for nb2 in 768 1024 1536 2048; do
+  echo "== nb2=$nb2"
+  GPR_NB2=$nb2 timeout -k 10 60 tools/gemm_bench 32768 768 2 2>&1 | grep -v "stamps\|sb0"
 done
-GPR_NB2=512 timeout -k 5 100 ./tools/gemm_bench 16384 0 2 | tail -4
-} > gpurun_out/nb2.log 2>&1
-cat gpurun_out/nb2.log

@@ -66,6 +66,12 @@ __device__ __forceinline__ double kexp_neg(double dist) {
 // Cody-Waite steps (n L1 exact: L1 has 32 significant bits, |n| < 2^19), |r| <= ln2/512,
 // exp(x) = 2^(n>>8) T[n&255] (1 + r p(r)) with a degree-5 Taylor p (truncation < 1e-20) and
 // T[j] = 2^(j/256) rounded once from extended precision on the host (ctx->dexptab).
+#ifndef GPR_KBUILD_MINB  // workgroups per CU the 16-B-store assembly kernels are compiled for
+#define GPR_KBUILD_MINB 2
+#endif
+#ifndef KB_CG  // columns per distance/exp group in kmat_tile_compute (2: 128 VGPRs,
+#define KB_CG 2  // 4 waves/SIMD; 8: 178 VGPRs, 2 waves/SIMD, SE+SE+WN 2.45 -> 2.20 ms)
+#endif
 __device__ __forceinline__ double kexp_neg_tab(double dist, const double* tab) {
 #ifdef GPR_KBUILD_NOEXP
   (void)tab;
@@ -347,31 +353,35 @@ __device__ __forceinline__ void kmat_tile_compute(const KParams& kp, const doubl
     for (int f = 0; f < NFILL; ++f)
       if (t + 256 * f < KT * D) lds[t + 256 * f] = fill[f];
     __syncthreads();
-    // 16 independent distance accumulators (8 columns x 2 rows), k outermost
-    double d0[8], d1[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) d0[c] = d1[c] = 0.0;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const double cv = lds[(cg + 8 * c) * D + k];
-        const double q0 = xr0[k] - cv, q1 = xr1[k] - cv;
-        d0[c] = fma(q0, q0, d0[c]);
-        d1[c] = fma(q1, q1, d1[c]);
-      }
-    }
     const double s2 = kp.sigma[p] * kp.sigma[p];
+    // columns in groups of KB_CG: KB_CG x 2 independent distance accumulators, k outermost
+    // (smaller groups keep fewer exp evaluations in flight: register pressure / occupancy)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      double t0 = s2 * kexp_neg_tab(d0[c], etab), t1 = s2 * kexp_neg_tab(d1[c], etab);
-      if (SYM) {
-        const int j = j0 + cg + 8 * c, i = i0 + 2 * l32;
-        if (i == j) t0 += kp.eps;
-        if (i + 1 == j) t1 += kp.eps;
+    for (int cb = 0; cb < 8; cb += KB_CG) {
+      double d0[KB_CG], d1[KB_CG];
+#pragma unroll
+      for (int c = 0; c < KB_CG; ++c) d0[c] = d1[c] = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+#pragma unroll
+        for (int c = 0; c < KB_CG; ++c) {
+          const double cv = lds[(cg + 8 * (cb + c)) * D + k];
+          const double q0 = xr0[k] - cv, q1 = xr1[k] - cv;
+          d0[c] = fma(q0, q0, d0[c]);
+          d1[c] = fma(q1, q1, d1[c]);
+        }
       }
-      v[c][0] = (p == 0) ? t0 : v[c][0] + t0;
-      v[c][1] = (p == 0) ? t1 : v[c][1] + t1;
+#pragma unroll
+      for (int c = 0; c < KB_CG; ++c) {
+        double t0 = s2 * kexp_neg_tab(d0[c], etab), t1 = s2 * kexp_neg_tab(d1[c], etab);
+        if (SYM) {
+          const int j = j0 + cg + 8 * (cb + c), i = i0 + 2 * l32;
+          if (i == j) t0 += kp.eps;
+          if (i + 1 == j) t1 += kp.eps;
+        }
+        v[cb + c][0] = (p == 0) ? t0 : v[cb + c][0] + t0;
+        v[cb + c][1] = (p == 0) ? t1 : v[cb + c][1] + t1;
+      }
     }
   }
   if (SYM && kp.has_noise) {
@@ -405,7 +415,7 @@ __device__ __forceinline__ void store_pair(double* K, size_t idx, bool ok0, bool
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void kmat_sym2_kernel(KParams kp, const double* __restrict__ xs,
+__global__ __launch_bounds__(256, GPR_KBUILD_MINB) void kmat_sym2_kernel(KParams kp, const double* __restrict__ xs,
                                                         int n, double* __restrict__ K, size_t ldk,
                                                         int ntiles) {
   __shared__ double lds[KT_LDS];
@@ -451,7 +461,7 @@ __global__ __launch_bounds__(256) void kmat_sym2_kernel(KParams kp, const double
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void kmat_cross2_kernel(KParams kp, const double* __restrict__ xs,
+__global__ __launch_bounds__(256, GPR_KBUILD_MINB) void kmat_cross2_kernel(KParams kp, const double* __restrict__ xs,
                                                           int n, const double* __restrict__ xps,
                                                           int m, double* __restrict__ K,
                                                           size_t ldk, int ntile_i, int ntiles) {

@@ -54,6 +54,25 @@ __device__ __forceinline__ bool tile_coords(const GemmK& a, int& m0, int& n0) {
   // flight (2G panels of 128 x K) stay in its 4 MB L2.  Placement only affects speed.
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
+  if (g.kend_from_m && !g.upper && !g.mask_upper) {
+    // triangular P: row-tile tm costs (tm + 1) K-steps.  Heavy rows first; with an even
+    // number of row tiles, block b and block b + T/2 (same XCD, and the pair that shares a
+    // CU when the grid is two workgroups per CU) get complementary rows tm + tm' = tiles_m - 1,
+    // so every CU carries the same K work.
+    const int tmn = a.tiles_m, tnn = a.tiles_n, half = (tmn / 2) * tnn;
+    if (bid >= tmn * tnn) return false;
+    int tm, tn;
+    if ((tmn & 1) == 0 && bid >= half) {
+      tm = (bid - half) / tnn;
+      tn = (bid - half) % tnn;
+    } else {
+      tm = tmn - 1 - bid / tnn;
+      tn = bid % tnn;
+    }
+    m0 = tm * TM;
+    n0 = tn * TN;
+    return true;
+  }
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int L = a.xcd_remap ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3)
                             : bid;
@@ -501,6 +520,7 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
     if (g.kfrom_n) flops = (double)g.M * g.M * g.M / 3.0;
   } else {
     nblk = (long long)a.super_m * super_n * a.gm * a.gn;
+    if (g.kend_from_m && !g.mask_upper) nblk = (long long)a.tiles_m * a.tiles_n;  // see tile_coords
     flops = 2.0 * g.M * (double)g.N * g.K;
     if (g.kend_from_m)  // upper-triangular P: row m of the product uses K-range [0, m]
       flops = (double)g.N * g.M * (g.M + 1);

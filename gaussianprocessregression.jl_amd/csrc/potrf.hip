@@ -1193,6 +1193,35 @@ int launch_diag(gpr_ctx* ctx, double* A, int lda, int n, int kglob, double* winv
   return 0;
 }
 
+// dst[r + c ldd] = src[r + c lds] for r < rows, c < cols: one workgroup per column chunk,
+// 16 B per lane when both sides allow it
+__global__ __launch_bounds__(256) void copy_panel_kernel(const double* __restrict__ src, size_t lds,
+                                                         double* __restrict__ dst, size_t ldd,
+                                                         int rows, int cols, int vec) {
+  typedef double d2c __attribute__((ext_vector_type(2)));
+  const int c = blockIdx.x;
+  if (c >= cols) return;
+  const double* sc = src + (size_t)c * lds;
+  double* dc = dst + (size_t)c * ldd;
+  if (vec) {
+    for (int r = 2 * threadIdx.x; r < rows; r += 512)
+      *reinterpret_cast<d2c*>(dc + r) = *reinterpret_cast<const d2c*>(sc + r);
+  } else {
+    for (int r = threadIdx.x; r < rows; r += 256) dc[r] = sc[r];
+  }
+}
+
+int launch_copy_panel(gpr_ctx* ctx, const double* src, int lds, double* dst, int ldd, int rows,
+                      int cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int vec = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0) && (lds % 2 == 0) &&
+                  (ldd % 2 == 0) && (rows % 2 == 0);
+  TimerScope ts(ctx, TC_OTHER, 0.0);
+  copy_panel_kernel<<<cols, 256, 0, ctx->ls>>>(src, (size_t)lds, dst, (size_t)ldd, rows, cols, vec);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
 hipEvent_t sync_event(gpr_ctx* ctx, size_t i) {
   while (ctx->sync_events.size() <= i) {
     hipEvent_t e;
@@ -1571,11 +1600,19 @@ int ensure_sq_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
 // norm_out is a deterministic post-pass over the solved B.
 static int trsm_ut_sq(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                       int ldb, double* norm_out, int lower_rhs) {
+  // One stream, per outer panel s: X_s = U_sq_s^{-T} B_s into a panel buffer (one GEMM with a
+  // per-tile K range, heavy/light tiles paired per CU), then ONE update GEMM of all rows below
+  // (B_rest -= U_s,rest^T X_s, K = nb2), then X_s copied back into B.  A lookahead stream for
+  // the next panel's solve measured no faster (the big update loses to the co-running
+  // kernels what the overlap gains) and was dropped.
   const int nb2 = ctx->sqinv_nb2;
-  hipStream_t s0 = ctx->stream, s1 = ctx->stream2;
+  hipStream_t s0 = ctx->stream;
+  ctx->ls = s0;
   auto cols = [&](int kend) { return lower_rhs ? std::min(nrhs, kend) : nrhs; };
   GPR_TRY(ensure_buf(ctx, &ctx->dpanel, &ctx->panel_cap, (size_t)nb2 * nrhs));
-  auto panel_solve = [&](int k, int kw, int nc) -> int {
+  for (int k = 0; k < n; k += nb2) {
+    const int kw = std::min(nb2, n - k), kend = k + kw;
+    const int nc = cols(kend);  // lower_rhs: columns >= kend of B_s are still zero
     GemmArgs g{};
     g.P = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2; g.ldp = kw;
     g.Q = dB + k; g.ldq = ldb;
@@ -1584,55 +1621,17 @@ static int trsm_ut_sq(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB
     g.alpha = 1.0; g.beta = 0.0;
     g.kend_from_m = 1;
     GPR_TRY(launch_gemm_tn(ctx, g, TC_TRSM_GEMM));
-    HIP_TRY(ctx, hipMemcpy2DAsync(dB + k, sizeof(double) * ldb, ctx->dpanel, sizeof(double) * kw,
-                                  sizeof(double) * kw, nc, hipMemcpyDeviceToDevice, ctx->ls));
-    return 0;
-  };
-  size_t ev = 0;
-  hipEvent_t e0 = sync_event(ctx, ev++);
-  HIP_TRY(ctx, hipEventRecord(e0, s0));
-  HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
-  ctx->ls = s1;
-  const int w0 = std::min(nb2, n);
-  int rc = panel_solve(0, w0, cols(w0));
-  hipEvent_t ev_p = sync_event(ctx, ev++);
-  hipEvent_t ev_b = nullptr;
-  if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
-  for (int k = 0; !rc && k + nb2 < n; k += nb2) {
-    const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
-    const int nc = cols(kend);
-    ctx->ls = s1;
-    if (ev_b && hipStreamWaitEvent(s1, ev_b, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
-    GemmArgs a{};
-    a.P = dU + k + (size_t)kend * ldu; a.ldp = ldu;
-    a.Q = dB + k; a.ldq = ldb;
-    a.C = dB + kend; a.ldc = ldb;
-    a.M = w2; a.N = nc; a.K = nb2;
-    a.alpha = -1.0; a.beta = 1.0;
-    if ((rc = launch_gemm_tn(ctx, a, TC_TRSM_GEMM))) break;
-    if ((rc = panel_solve(kend, w2, cols(rest0)))) break;
-    hipEvent_t ev_p_next = sync_event(ctx, ev++);
-    if (hipEventRecord(ev_p_next, s1) != hipSuccess) { rc = GPR_E_HIP; break; }
-    ctx->ls = s0;
-    if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
-    if (rest0 < n) {
+    if (kend < n) {
       GemmArgs b{};
-      b.P = dU + k + (size_t)rest0 * ldu; b.ldp = ldu;
-      b.Q = dB + k; b.ldq = ldb;
-      b.C = dB + rest0; b.ldc = ldb;
-      b.M = n - rest0; b.N = nc; b.K = nb2;
+      b.P = dU + k + (size_t)kend * ldu; b.ldp = ldu;
+      b.Q = ctx->dpanel; b.ldq = kw;
+      b.C = dB + kend; b.ldc = ldb;
+      b.M = n - kend; b.N = nc; b.K = kw;
       b.alpha = -1.0; b.beta = 1.0;
-      if ((rc = launch_gemm_tn(ctx, b, TC_TRSM_GEMM))) break;
+      GPR_TRY(launch_gemm_tn(ctx, b, TC_TRSM_GEMM));
     }
-    ev_b = sync_event(ctx, ev++);
-    if (hipEventRecord(ev_b, s0) != hipSuccess) { rc = GPR_E_HIP; break; }
-    ev_p = ev_p_next;
+    GPR_TRY(launch_copy_panel(ctx, ctx->dpanel, kw, dB + k, ldb, kw, nc));
   }
-  ctx->ls = s0;
-  hipEvent_t ej = sync_event(ctx, ev++);
-  HIP_TRY(ctx, hipEventRecord(ej, s1));
-  HIP_TRY(ctx, hipStreamWaitEvent(s0, ej, 0));
-  if (rc) return rc;
   if (norm_out) {
     TimerScope ts(ctx, TC_OTHER, 0.0);
     colnorm_sub_kernel<<<(nrhs + 3) / 4, 256, 0, s0>>>(dB, (size_t)ldb, n, nrhs, norm_out);

@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 #include "../gaussianprocessregression.jl_amd/csrc/common.hpp"
 
@@ -89,6 +90,87 @@ int main(int argc, char** argv) {
       double ms, fl; long long ln;
       gpr_timing_get(ctx, c, &ms, &ln, &fl);
       if (ln) printf("  %-6s %8.2f ms %5lld launches %7.2f TF\n", nm[c], ms, ln, fl / ms / 1e9);
+    }
+    return 0;
+  }
+  if (mode == 4) {
+    // posterior TRSM in context: K (SE+SE+WN) -> potrf -> Kpx (N x K cross) -> U^-T Kpx
+    const int d = 8, np = K;
+    double *X, *A, *B;
+    hipMalloc(&X, sizeof(double) * d * (N + np));
+    hipMalloc(&A, sizeof(double) * (size_t)N * N);
+    hipMalloc(&B, sizeof(double) * (size_t)N * np);
+    init_kernel<<<1024, 256, 0, s>>>(X, (size_t)d * (N + np), 7);
+    int kinds[3] = {GPR_SE, GPR_SE, GPR_WN};
+    std::vector<double> hp(2 * (d + 1) + 1, 3.0);
+    hp[0] = 1.0; hp[d + 1] = 1.0; hp[2 * (d + 1)] = 0.1;
+    gpr_kernel(ctx, kinds, 3, hp.data(), d, X, N, nullptr, N, 1, 1e-8, A, N);
+    int info = 0;
+    gpr_potrf_upper(ctx, A, N, N, &info);
+    printf("potrf info=%d\n", info);
+    for (int rep = 0; rep < 3; ++rep) {
+      gpr_kernel(ctx, kinds, 3, hp.data(), d, X, N, X + (size_t)d * N, np, 0, 1e-8, B, N);
+      gpr_timing_reset(ctx);
+      gpr_timing_enable(ctx, 1);
+      hipEventRecord(e0, s);
+      trsm_ut_core(ctx, A, N, N, B, np, N, nullptr, 0);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+      float ms; hipEventElapsedTime(&ms, e0, e1);
+      printf("trsm N=%d nrhs=%d: %.2f ms  %.2f TFLOP/s\n", N, np, ms, (double)N * N * np / ms / 1e9);
+      const char* nm[6] = {"kbuild", "syrk", "panel", "trsm", "other", "gemm_pipe"};
+      for (int c = 0; c < 6; ++c) {
+        double tms, fl; long long ln;
+        gpr_timing_get(ctx, c, &tms, &ln, &fl);
+        if (ln) printf("  %-9s %8.2f ms %5lld launches %7.2f TF\n", nm[c], tms, ln, fl / tms / 1e9);
+      }
+    }
+    return 0;
+  }
+  if (mode == 3) {
+    // general C (M x N, ldc) -= P^T Q with P K x M (ldp), Q K x N (ld K): TRSM-update shapes
+    const int M = argc > 4 ? atoi(argv[4]) : N;
+    const int ldp = argc > 5 ? atoi(argv[5]) : K;
+    const int ldc = argc > 6 ? atoi(argv[6]) : M;
+    double *P3, *Q3, *C3;
+    hipMalloc(&P3, sizeof(double) * (size_t)ldp * M);
+    hipMalloc(&Q3, sizeof(double) * (size_t)K * N);
+    hipMalloc(&C3, sizeof(double) * (size_t)ldc * N);
+    init_kernel<<<1024, 256, 0, s>>>(P3, (size_t)ldp * M, 1);
+    init_kernel<<<1024, 256, 0, s>>>(Q3, (size_t)K * N, 3);
+    init_kernel<<<1024, 256, 0, s>>>(C3, (size_t)ldc * N, 2);
+    if (getenv("GEMM_KDATA")) {
+      // kernel-matrix data (smooth, wide exponent range) instead of uniform random
+      const int d = 8, npt = std::max(std::max(ldp, ldc), std::max(M, N));
+      double* X;
+      hipMalloc(&X, sizeof(double) * d * npt);
+      init_kernel<<<1024, 256, 0, s>>>(X, (size_t)d * npt, 7);
+      int kinds[2] = {GPR_SE, GPR_WN};
+      std::vector<double> hp(d + 2, 3.0);
+      hp[0] = 1.0; hp[d + 1] = 0.1;
+      gpr_kernel(ctx, kinds, 2, hp.data(), d, X, ldp, X, M, 0, 1e-8, P3, ldp);
+      gpr_kernel(ctx, kinds, 2, hp.data(), d, X, ldc, X, N, 0, 1e-8, C3, ldc);
+      gpr_kernel(ctx, kinds, 2, hp.data(), d, X, K, X, N, 0, 1e-8, Q3, K);
+      hipStreamSynchronize(s);
+    }
+    GemmArgs g{};
+    g.P = P3; g.ldp = ldp; g.Q = Q3; g.ldq = K; g.C = C3; g.ldc = ldc;
+    g.M = M; g.N = N; g.K = K; g.alpha = -1.0; g.beta = 1.0;
+    const double flops = 2.0 * M * (double)N * K;
+    const int reps = getenv("GEMM_REPS") ? atoi(getenv("GEMM_REPS")) : 5;
+    std::vector<hipEvent_t> ev(reps + 1);
+    for (auto& e : ev) hipEventCreate(&e);
+    // back to back (sustained clock), one event between launches
+    hipEventRecord(ev[0], s);
+    for (int rep = 0; rep < reps; ++rep) {
+      launch_gemm_tn(ctx, g, TC_OTHER);
+      hipEventRecord(ev[rep + 1], s);
+    }
+    hipEventSynchronize(ev[reps]);
+    for (int rep = 0; rep < reps; ++rep) {
+      float ms; hipEventElapsedTime(&ms, ev[rep], ev[rep + 1]);
+      if (rep >= 2 && (rep < 6 || rep % 10 == 0 || rep == reps - 1))
+        printf("gemm M=%d N=%d K=%d ldp=%d ldc=%d rep %d: %.3f ms  %.2f TFLOP/s\n", M, N, K, ldp, ldc, rep, ms, flops / ms / 1e9);
     }
     return 0;
   }

@@ -40,12 +40,14 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK = 78.6      # TFLOP/s, FP64 matrix spec (measured 77.7 in tools/probe)
-DOMINANT_KERNEL = "gemm_tn_pipe8_kernel"
+# the pipelined FP64 GEMM: two compiled variants of one kernel (beta != 0 preloads C, `z`
+# starts from zero); timing class 5 counts every launch of both
+DOMINANT_KERNELS = ("gemm_tn_pipe8_kernel", "gemm_tn_pipe8z_kernel")
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 
 
-def pmc_traffic(kernel, n, npred):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+def pmc_traffic(kernels, n, npred):
+    """HBM bytes per launch (dispatch-weighted over `kernels`) from the newest committed PMC summary
     (profiles/rNN_pmc_summary.json, written by tools/profile_round.sh from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command, FETCH_SIZE
     doubled per the gfx950 16-B/lane correction).  None when no summary matches."""
@@ -59,9 +61,13 @@ def pmc_traffic(kernel, n, npred):
                 js = json.load(fh)
         except (OSError, ValueError):
             continue
-        k = js.get("kernels", {}).get(kernel)
-        if k and js.get("config", {}).get("N") == n and js.get("config", {}).get("np") == npred:
-            return k.get("traffic_bytes_per_launch")
+        if js.get("config", {}).get("N") != n or js.get("config", {}).get("np") != npred:
+            continue
+        ks = [js.get("kernels", {}).get(k) for k in kernels]
+        if not all(ks):
+            continue
+        w = [k.get("trace", {}).get("calls") or k.get("dispatches_fetch_pass") or 1 for k in ks]
+        return sum(wi * k["traffic_bytes_per_launch"] for wi, k in zip(w, ks)) / sum(w)
     return None
 
 
@@ -246,7 +252,7 @@ def main():
     # timed per launch with HIP events on the stream it is launched on (timing class 5)
     g_ms, g_launch, g_fl = cls["gemm_pipe"]
     achieved = g_fl / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
-    traffic = pmc_traffic(DOMINANT_KERNEL, N, NP)
+    traffic = pmc_traffic(DOMINANT_KERNELS, N, NP)
 
     out = None
     if rank == 0:
@@ -273,7 +279,7 @@ def main():
             "stage_ms": stg,
             "syrk_TFLOPs": cls["syrk"][2] / (cls["syrk"][0] * 1e-3) / 1e12 if cls["syrk"][0] else None,
             "roofline": {
-                "kernel": DOMINANT_KERNEL,
+                "kernel": " + ".join(DOMINANT_KERNELS),
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": FP64_MFMA_PEAK,

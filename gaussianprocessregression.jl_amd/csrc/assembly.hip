@@ -59,38 +59,19 @@ __device__ __forceinline__ double kexp_neg(double dist) {
 #endif
 }
 
-// exp(-dist) for the 16-B-store kernels: Tang's table method, ~1 ulp (the ocml exp costs ~28
-// instructions with its range checks and quarter-rate conversions and made K-assembly
-// VALU-bound at two SE parts).  x = -dist clamped at -800 (exp underflows to 0 long before;
-// a NaN dist fails the compare and propagates), n = rint(x 256/ln2), r = x - n ln2/256 in two
-// Cody-Waite steps (n L1 exact: L1 has 32 significant bits, |n| < 2^19), |r| <= ln2/512,
-// exp(x) = 2^(n>>8) T[n&255] (1 + r p(r)) with a degree-5 Taylor p (truncation < 1e-20) and
+// The 16-B-store kernels evaluate exp(-dist) by Tang's table method, ~1 ulp (kexp_s2 below;
+// the ocml exp costs ~28 instructions with its range checks and quarter-rate conversions and
+// made K-assembly VALU-bound at two SE parts).  x = -dist clamped at -800 (exp underflows to 0
+// long before; a NaN dist fails the compare and propagates), n = rint(x 256/ln2),
+// r = x - n ln2/256 in two Cody-Waite steps (n L1 exact: L1 has 32 significant bits,
+// |n| < 2^19), |r| <= ln2/512, exp(x) = 2^(n>>8) T[n&255] (1 + expm1(r)), with
 // T[j] = 2^(j/256) rounded once from extended precision on the host (ctx->dexptab).
 #ifndef GPR_KBUILD_MINB  // workgroups per CU the 16-B-store assembly kernels are compiled for
-#define GPR_KBUILD_MINB 2
+#define GPR_KBUILD_MINB 4
 #endif
 #ifndef KB_CG  // columns per distance/exp group in kmat_tile_compute (2: 128 VGPRs,
 #define KB_CG 2  // 4 waves/SIMD; 8: 178 VGPRs, 2 waves/SIMD, SE+SE+WN 2.45 -> 2.20 ms)
 #endif
-__device__ __forceinline__ double kexp_neg_tab(double dist, const double* tab) {
-#ifdef GPR_KBUILD_NOEXP
-  (void)tab;
-  return fma(dist, -1e-3, 1.0);
-#else
-  const double x = dist > 800.0 ? -800.0 : -dist;
-  const double nf = __builtin_rint(x * 369.3299304675746);
-  double r = fma(nf, -0.00270760617331689, x);
-  r = fma(nf, -7.453964567463233e-13, r);
-  const int ni = (int)nf;
-  double p = fma(r, 0.008333333333333333, 0.041666666666666664);
-  p = fma(r, p, 0.16666666666666666);
-  p = fma(r, p, 0.5);
-  p = fma(r, p, 1.0);
-  const double t = tab[ni & 255];
-  return __builtin_ldexp(fma(t, r * p, t), ni >> 8);
-#endif
-}
-
 // D = sum_k (xr_k - xc_k)^2 with xr in registers and xc wave-uniform (scalar loads).
 template <int D>
 __device__ __forceinline__ double sqdist(const double* xr, const double* __restrict__ xc,
@@ -322,10 +303,56 @@ int scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, doubl
 // conflict-free scalar writes) and is re-read as row pairs, so it too is stored 16 B/lane.
 constexpr int KT_LDS = KT * (KT + 1);  // doubles; also holds the 64 x D column points
 
-template <int D, bool SYM>
+#ifndef GPR_EXP32  // 1: 32-entry exp tables (conflict-free LDS gathers, 2 more FMAs)
+#define GPR_EXP32 0
+#endif
+// s2 * exp(-dist) with the part's table ts[j] = s2 * 2^(j/256): the Tang reduction of
+// kexp_neg_tab with magic-constant rounding (kf = x 256/ln2 + 1.5 2^52 holds n = rint(x 256/ln2)
+// in its low word: no rndne / cvt), a degree-4 expm1 (truncation < 0.2 ulp) and sigma^2 folded
+// into the table (one rounding of s2 * T[j]).  16 VALU + 1 LDS read per element.
+__device__ __forceinline__ double kexp_s2(double dist, const double* ts) {
+#ifdef GPR_KBUILD_NOEXP
+  return ts[0] * fma(dist, -1e-3, 1.0);
+#elif GPR_EXP32
+  // 32-entry table 2^(j/32) (every entry in its own LDS bank pair: conflict-free gathers),
+  // |r| <= ln2/64, degree-6 expm1 (truncation < 0.03 ulp); tab[j] = ts[8 j]
+  const double x = dist > 800.0 ? -800.0 : -dist;
+  const double kf = fma(x, 46.16624130844683, 6755399441055744.0);
+  const double nf = kf - 6755399441055744.0;
+  double r = fma(nf, -0.02166084938653512, x);  // ln2/32 = L1 (32 bits) + L2
+  r = fma(nf, -5.9631716539705866e-12, r);
+  const int ni = (int)(unsigned)__double_as_longlong(kf);
+  double p = fma(r, 1.3888888888888889e-03, 8.3333333333333332e-03);
+  p = fma(r, p, 0.041666666666666664);
+  p = fma(r, p, 0.16666666666666666);
+  p = fma(r, p, 0.5);
+  p = r * p;
+  const double q = fma(r, p, r);
+  const double t = ts[ni & 31];
+  return __builtin_ldexp(fma(t, q, t), ni >> 5);
+#else
+  const double x = dist > 800.0 ? -800.0 : -dist;
+  const double kf = fma(x, 369.3299304675746, 6755399441055744.0);
+  const double nf = kf - 6755399441055744.0;
+  double r = fma(nf, -0.00270760617331689, x);
+  r = fma(nf, -7.453964567463233e-13, r);
+  const int ni = (int)(unsigned)__double_as_longlong(kf);
+  double p = fma(r, 0.041666666666666664, 0.16666666666666666);
+  p = fma(r, p, 0.5);
+  p = r * p;
+  const double q = fma(r, p, r);  // expm1(r)
+  const double t = ts[ni & 255];
+  return __builtin_ldexp(fma(t, q, t), ni >> 8);
+#endif
+}
+
+// One 64 x 64 tile of K (or cross K), all SE parts summed in part order (src/compose_covar.jl:
+// 52-56).  DIAG: a diagonal tile of the symmetric K -- eps per SE part and sigma_n^2 on i == j
+// (only these 1/nt of the tiles pay the index compares).  tabs = nse tables of 256 doubles.
+template <int D, bool DIAG>
 __device__ __forceinline__ void kmat_tile_compute(const KParams& kp, const double* __restrict__ xs,
                                                   int n, const double* __restrict__ xcs, int m,
-                                                  int i0, int j0, double* lds, const double* etab,
+                                                  int i0, int j0, double* lds, const double* tabs,
                                                   double (&v)[8][2]) {
   constexpr int NFILL = (KT * D + 255) / 256;  // column-point doubles per thread per part
   const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
@@ -353,7 +380,7 @@ __device__ __forceinline__ void kmat_tile_compute(const KParams& kp, const doubl
     for (int f = 0; f < NFILL; ++f)
       if (t + 256 * f < KT * D) lds[t + 256 * f] = fill[f];
     __syncthreads();
-    const double s2 = kp.sigma[p] * kp.sigma[p];
+    const double* ts = tabs + 256 * p;
     // columns in groups of KB_CG: KB_CG x 2 independent distance accumulators, k outermost
     // (smaller groups keep fewer exp evaluations in flight: register pressure / occupancy)
 #pragma unroll
@@ -373,18 +400,18 @@ __device__ __forceinline__ void kmat_tile_compute(const KParams& kp, const doubl
       }
 #pragma unroll
       for (int c = 0; c < KB_CG; ++c) {
-        double t0 = s2 * kexp_neg_tab(d0[c], etab), t1 = s2 * kexp_neg_tab(d1[c], etab);
-        if (SYM) {
+        double t0 = kexp_s2(d0[c], ts), t1 = kexp_s2(d1[c], ts);
+        if (DIAG) {
           const int j = j0 + cg + 8 * (cb + c), i = i0 + 2 * l32;
           if (i == j) t0 += kp.eps;
           if (i + 1 == j) t1 += kp.eps;
         }
-        v[cb + c][0] = (p == 0) ? t0 : v[cb + c][0] + t0;
-        v[cb + c][1] = (p == 0) ? t1 : v[cb + c][1] + t1;
+        v[cb + c][0] += t0;  // 0 + t == t: part 1 enters unrounded
+        v[cb + c][1] += t1;
       }
     }
   }
-  if (SYM && kp.has_noise) {
+  if (DIAG && kp.has_noise) {
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int j = j0 + cg + 8 * c, i = i0 + 2 * l32;
@@ -392,6 +419,16 @@ __device__ __forceinline__ void kmat_tile_compute(const KParams& kp, const doubl
       if (i + 1 == j) v[c][1] += kp.noise2;
     }
   }
+}
+
+// per-part exp tables s2_p * 2^(j/256) into LDS (256 threads)
+__device__ __forceinline__ void load_part_tables(const KParams& kp, double* tabs) {
+#if GPR_EXP32
+  const double T = kp.exptab[(threadIdx.x & 31) << 3];  // compact 2^(j/32) tables
+#else
+  const double T = kp.exptab[threadIdx.x];
+#endif
+  for (int p = 0; p < kp.nse; ++p) tabs[256 * p + threadIdx.x] = (kp.sigma[p] * kp.sigma[p]) * T;
 }
 
 typedef double kd2 __attribute__((ext_vector_type(2)));
@@ -418,10 +455,11 @@ template <int D>
 __global__ __launch_bounds__(256, GPR_KBUILD_MINB) void kmat_sym2_kernel(KParams kp, const double* __restrict__ xs,
                                                         int n, double* __restrict__ K, size_t ldk,
                                                         int ntiles) {
-  __shared__ double lds[KT_LDS];
-  __shared__ double etab[256];
+  extern __shared__ double dyn_lds[];  // KT_LDS doubles, then nse exp tables
+  double* lds = dyn_lds;
+  double* tabs = dyn_lds + KT_LDS;
   const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
-  etab[t] = kp.exptab[t];
+  load_part_tables(kp, tabs);
   __syncthreads();
   // persistent: a workgroup walks tiles, so one tile's math overlaps the previous tile's
   // stores draining to HBM
@@ -432,7 +470,10 @@ __global__ __launch_bounds__(256, GPR_KBUILD_MINB) void kmat_sym2_kernel(KParams
     const int bi = bid - bj * (bj + 1) / 2;
     const int i0 = bi * KT, j0 = bj * KT;
     double v[8][2];
-    kmat_tile_compute<D, true>(kp, xs, n, xs, n, i0, j0, lds, etab, v);
+    if (bi == bj)
+      kmat_tile_compute<D, true>(kp, xs, n, xs, n, i0, j0, lds, tabs, v);
+    else
+      kmat_tile_compute<D, false>(kp, xs, n, xs, n, i0, j0, lds, tabs, v);
     const int i = i0 + 2 * l32;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -465,16 +506,17 @@ __global__ __launch_bounds__(256, GPR_KBUILD_MINB) void kmat_cross2_kernel(KPara
                                                           int n, const double* __restrict__ xps,
                                                           int m, double* __restrict__ K,
                                                           size_t ldk, int ntile_i, int ntiles) {
-  __shared__ double lds[KT * D];
-  __shared__ double etab[256];
+  extern __shared__ double dyn_lds[];  // KT * D doubles, then nse exp tables
+  double* lds = dyn_lds;
+  double* tabs = dyn_lds + KT * D;
   const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
-  etab[t] = kp.exptab[t];
+  load_part_tables(kp, tabs);
   __syncthreads();
   for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
     const int bi = bid % ntile_i, bj = bid / ntile_i;
     const int i0 = bi * KT, j0 = bj * KT;
     double v[8][2];
-    kmat_tile_compute<D, false>(kp, xs, n, xps, m, i0, j0, lds, etab, v);
+    kmat_tile_compute<D, false>(kp, xs, n, xps, m, i0, j0, lds, tabs, v);
     const int i = i0 + 2 * l32;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -491,7 +533,8 @@ void launch_sym(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double
   if constexpr (D > 0) {
     if (vec_store_ok(K, ldk)) {
       const int grid = (int)std::min<long long>(nblk, kbuild_grid());
-      kmat_sym2_kernel<D><<<grid, 256, 0, ctx->stream>>>(kp, xs, n, K, (size_t)ldk, (int)nblk);
+      const size_t lds_bytes = sizeof(double) * (KT_LDS + 256 * kp.nse);
+      kmat_sym2_kernel<D><<<grid, 256, lds_bytes, ctx->stream>>>(kp, xs, n, K, (size_t)ldk, (int)nblk);
       return;
     }
   }
@@ -506,12 +549,322 @@ void launch_cross(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, cons
   if constexpr (D > 0) {
     if (vec_store_ok(K, ldk)) {
       const int grid = (int)std::min<long long>(nblk, kbuild_grid());
-      kmat_cross2_kernel<D><<<grid, 256, 0, ctx->stream>>>(kp, xs, n, xps, m, K, (size_t)ldk, nti,
-                                                           (int)nblk);
+      const size_t lds_bytes = sizeof(double) * (KT * D + 256 * kp.nse);
+      kmat_cross2_kernel<D><<<grid, 256, lds_bytes, ctx->stream>>>(kp, xs, n, xps, m, K, (size_t)ldk,
+                                                                   nti, (int)nblk);
       return;
     }
   }
   kmat_cross_kernel<D><<<nblk, 256, 0, ctx->stream>>>(kp, xs, n, xps, m, K, (size_t)ldk, nti);
+}
+
+// ---- Gram form of the distance on FP64 MFMA ---------------------------------------------
+// -D_ab = (-|y_a|^2 - |y_b|^2) + sum_k (2 y_a,k) y_b,k with y = x .* l - c, where c is the mean of
+// the part's scaled training points (distances are translation invariant; centring keeps |y|^2,
+// the cancelling terms, small).  Per 16 x 16 block the sum is ceil(d/4) v_mfma_f64_16x16x4f64
+// started from C = -|y_a|^2 - |y_b|^2 (one VALU add per element), so the FP64 VALU is left with
+// exp (kexp_s2) and the part sum.  Rounding: |error of D| <~ (d + 1) u (|y_a|^2 + |y_b|^2),
+// ~1e-15 absolute at the default hp (K within rtol 1e-13 of the reference's difference form,
+// tests/test_gpu_parity.py); a same-object diagonal gets D = 0 exactly and diagonal tiles are
+// made bitwise symmetric.  GPR_KBUILD_EXACT=1 selects the reference's difference form
+// (x .* l - x' .* l)^2 in kmat_sym2/cross2.
+// Measured (tools/kbuild_bench, SE+SE+WN N = 32768 d = 8, same box): difference form 2.43 ms,
+// the same Gram sum on the VALU 2.36 ms, MFMA with the norms as a third k-step 2.07 ms.
+// Operands are prepared once per call in MFMA lane order: for 16-point block b and k-step s,
+// 64 doubles, lane l <-> (point 16 b + (l & 15), k = 4 s + (l >> 4)) -- every operand load is one
+// coalesced 512-B wave load; points padded to a multiple of 64 (zeros).
+typedef double gd4 __attribute__((ext_vector_type(4)));
+#ifndef GRAM_EXPG  // exp evaluations the scheduler may interleave (register pressure)
+#define GRAM_EXPG 4
+#endif
+
+// grid = nse * d workgroups of 256: c[p][k] = mean_a xs[p][a][k] (fixed-order tree sum)
+__global__ __launch_bounds__(256) void gram_center_kernel(const double* __restrict__ xs, int n,
+                                                          int d, double* __restrict__ c) {
+  __shared__ double red[256];
+  const int p = blockIdx.x / d, k = blockIdx.x % d;
+  double sum = 0.0;
+  for (int a = threadIdx.x; a < n; a += 256) sum += xs[((size_t)p * n + a) * d + k];
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) c[p * KMAXD + k] = red[0] / (double)n;
+}
+
+// out[p][blk][s][lane] = scale * y[16 blk + (lane & 15)][4 s + (lane >> 4)] (0 past d or n);
+// nrm[p][a] = -|y_a|^2 (0 for padded points)
+__global__ void gram_prep_kernel(const double* __restrict__ xs, int n, int d, int S, int nblk,
+                                 int nse, const double* __restrict__ c, double scale,
+                                 double* __restrict__ out, double* __restrict__ nrm) {
+  const size_t total = (size_t)nse * nblk * S * 64;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(t & 63);
+    const size_t r = t >> 6;
+    const int s = (int)(r % S);
+    const size_t r2 = r / S;
+    const int blk = (int)(r2 % nblk), p = (int)(r2 / nblk);
+    const int a = blk * 16 + (lane & 15), k = 4 * s + (lane >> 4);
+    const double* xa = xs + ((size_t)p * n + a) * d;
+    const double* cp = c + p * KMAXD;
+    out[t] = (a < n && k < d) ? scale * (xa[k] - cp[k]) : 0.0;
+    if (nrm && s == 0 && lane < 16) {
+      double q = 0.0;
+      if (a < n)
+        for (int kk = 0; kk < d; ++kk) {
+          const double y = xa[kk] - cp[kk];
+          q = fma(y, y, q);
+        }
+      nrm[(size_t)p * nblk * 16 + a] = -q;
+    }
+  }
+}
+
+// One 64 x 64 tile of K on MFMA + VALU, SE parts summed in order.  Wave w owns the 32 x 32
+// quadrant (rows 32 (w & 1), cols 32 (w >> 1)): 2 x 2 blocks of 16 x 16; lane l / register q of
+// block (rb, cb) <-> row 16 rb + (l >> 4) + 4 q, col 16 cb + (l & 15).
+template <int S, bool DIAG>
+__device__ __forceinline__ void gram_tile(const KParams& kp, const double* __restrict__ gA,
+                                          const double* __restrict__ gB, const double* __restrict__ nA,
+                                          const double* __restrict__ nB, int nblkA, int nblkB,
+                                          int i0, int j0, const double* tabs, gd4 (&v)[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w & 1, wc = w >> 1;
+  const int ba = (i0 >> 4) + 2 * wr, bb = (j0 >> 4) + 2 * wc;  // first 16-blocks
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) v[rb][cb] = gd4{0.0, 0.0, 0.0, 0.0};
+  for (int p = 0; p < kp.nse; ++p) {
+    const double* Ap = gA + ((size_t)p * nblkA + ba) * S * 64 + lane;
+    const double* Bp = gB + ((size_t)p * nblkB + bb) * S * 64 + lane;
+    const double* nAp = nA + (size_t)p * nblkA * 16 + ba * 16 + (lane >> 4);
+    const double* nBp = nB + (size_t)p * nblkB * 16 + bb * 16 + (lane & 15);
+    double a[2][S], b[2][S], nr[2][4], nc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        a[h][s] = Ap[(h * S + s) * 64];
+        b[h][s] = Bp[(h * S + s) * 64];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nr[h][q] = nAp[16 * h + 4 * q];
+      nc[h] = nBp[16 * h];
+    }
+    gd4 acc[2][2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[rb][cb][q] = nr[rb][q] + nc[cb];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          acc[rb][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rb][s], b[cb][s], acc[rb][cb], 0, 0, 0);
+      }
+    const double* ts = tabs + 256 * p;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double x = acc[rb][cb][q];  // -D
+          bool on_diag = false;
+          if (DIAG) {
+            on_diag = wr == wc && rb == cb && (lane >> 4) + 4 * q == (lane & 15);
+            if (on_diag) x = 0.0;
+          }
+          double t = kexp_s2(-x, ts);
+          if (DIAG && on_diag) t += kp.eps;
+          v[rb][cb][q] += t;
+          if ((q + 1) % GRAM_EXPG == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+  }
+  if (DIAG && kp.has_noise && wr == wc) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if ((lane >> 4) + 4 * q == (lane & 15)) v[rb][rb][q] += kp.noise2;
+  }
+}
+
+// tile -> LDS, column-major with column stride 65
+__device__ __forceinline__ void gram_to_lds(const gd4 (&v)[2][2], double* T) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = 32 * (w & 1) + (lane >> 4), c0 = 32 * (w >> 1) + (lane & 15);
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) T[(c0 + 16 * cb) * (KT + 1) + r0 + 16 * rb + 4 * q] = v[rb][cb][q];
+}
+
+// upper-triangle tile bid -> (bi <= bj), column-by-column order; wave-uniform
+__device__ __forceinline__ void tri_tile(int bid, int* bi, int* bj) {
+  int j = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+  while ((j + 1) * (j + 2) / 2 <= bid) ++j;
+  while (j * (j + 1) / 2 > bid) --j;
+  j = __builtin_amdgcn_readfirstlane(j);
+  *bj = j;
+  *bi = __builtin_amdgcn_readfirstlane(bid - j * (j + 1) / 2);
+}
+
+template <int S>
+__global__ __launch_bounds__(256, 4) void kmat_symg_kernel(KParams kp, const double* __restrict__ gA,
+                                                         const double* __restrict__ gB,
+                                                         const double* __restrict__ nrm, int nblk,
+                                                         int n, double* __restrict__ K, size_t ldk,
+                                                         int ntiles) {
+  extern __shared__ double dyn_lds[];  // KT_LDS doubles (tile), then nse exp tables
+  double* T = dyn_lds;
+  double* tabs = dyn_lds + KT_LDS;
+  const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
+  load_part_tables(kp, tabs);
+  __syncthreads();
+  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+    int bi, bj;
+    tri_tile(bid, &bi, &bj);
+    const int i0 = bi * KT, j0 = bj * KT;
+    gd4 v[2][2];
+    if (bi == bj)
+      gram_tile<S, true>(kp, gA, gB, nrm, nrm, nblk, nblk, i0, j0, tabs, v);
+    else
+      gram_tile<S, false>(kp, gA, gB, nrm, nrm, nblk, nblk, i0, j0, tabs, v);
+    __syncthreads();  // previous tile's LDS reads are done
+    gram_to_lds(v, T);
+    __syncthreads();
+    // direct: K[i0 + 2 l32 + {0,1}, j0 + jl] = T[jl][2 l32 + {0,1}]
+    const int i = i0 + 2 * l32;
+    if (bi == bj) {
+      // diagonal tile: the strictly-lower half mirrors the upper, so K == K^T bitwise
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int jl = cg + 8 * c, j = j0 + jl, r0 = 2 * l32, r1 = 2 * l32 + 1;
+        const double e0 = r0 <= jl ? T[jl * (KT + 1) + r0] : T[r0 * (KT + 1) + jl];
+        const double e1 = r1 <= jl ? T[jl * (KT + 1) + r1] : T[r1 * (KT + 1) + jl];
+        if (j < n) store_pair(K, (size_t)i + (size_t)j * ldk, i < n, i + 1 < n, e0, e1);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int jl = cg + 8 * c, j = j0 + jl;
+      if (j < n)
+        store_pair(K, (size_t)i + (size_t)j * ldk, i < n, i + 1 < n, T[jl * (KT + 1) + 2 * l32],
+                   T[jl * (KT + 1) + 2 * l32 + 1]);
+    }
+    // mirror: K[j0 + 2 l32 + {0,1}, i0 + il] = tile(il, 2 l32 + {0,1}) = T[2 l32 + {0,1}][il]
+    const int jj = j0 + 2 * l32;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int il = cg + 8 * c;
+      if (i0 + il < n)
+        store_pair(K, (size_t)jj + (size_t)(i0 + il) * ldk, jj < n, jj + 1 < n,
+                   T[(2 * l32) * (KT + 1) + il], T[(2 * l32 + 1) * (KT + 1) + il]);
+    }
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(256, 4) void kmat_crossg_kernel(KParams kp, const double* __restrict__ gA,
+                                                           const double* __restrict__ gB,
+                                                           const double* __restrict__ nrmA,
+                                                           const double* __restrict__ nrmB,
+                                                           int nblkA, int nblkB, int n, int m,
+                                                           double* __restrict__ K, size_t ldk,
+                                                           int ntile_i, int ntiles) {
+  extern __shared__ double dyn_lds[];
+  double* T = dyn_lds;
+  double* tabs = dyn_lds + KT_LDS;
+  const int t = threadIdx.x, l32 = t & 31, cg = t >> 5;
+  load_part_tables(kp, tabs);
+  __syncthreads();
+  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+    const int bi = __builtin_amdgcn_readfirstlane(bid % ntile_i);
+    const int bj = __builtin_amdgcn_readfirstlane(bid / ntile_i);
+    const int i0 = bi * KT, j0 = bj * KT;
+    gd4 v[2][2];
+    gram_tile<S, false>(kp, gA, gB, nrmA, nrmB, nblkA, nblkB, i0, j0, tabs, v);
+    __syncthreads();
+    gram_to_lds(v, T);
+    __syncthreads();
+    const int i = i0 + 2 * l32;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int jl = cg + 8 * c, j = j0 + jl;
+      if (j < m)
+        store_pair(K, (size_t)i + (size_t)j * ldk, i < n, i + 1 < n, T[jl * (KT + 1) + 2 * l32],
+                   T[jl * (KT + 1) + 2 * l32 + 1]);
+    }
+  }
+}
+
+inline bool gram_enabled(int d) {
+  static const bool exact = getenv("GPR_KBUILD_EXACT") != nullptr;
+  return !exact && d <= 4 * 5;
+}
+
+template <int S>
+int launch_gram(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const double* xps,
+                int m, int same, double* K, int ldk) {
+  const int d = kp.d;
+  const int nbA = ((n + KT - 1) / KT) * (KT / 16);
+  const int nbB = same ? nbA : ((m + KT - 1) / KT) * (KT / 16);
+  const size_t opA = (size_t)kp.nse * nbA * S * 64, opB = same ? 0 : (size_t)kp.nse * nbB * S * 64;
+  const size_t nA = (size_t)kp.nse * nbA * 16, nB = same ? 0 : (size_t)kp.nse * nbB * 16;
+  // dgA: row operands + row norms; dgB: column operands + column norms (cross only)
+  GPR_TRY(ensure_buf(ctx, &ctx->dgc, &ctx->gc_cap, (size_t)KMAXP * KMAXD));
+  GPR_TRY(ensure_buf(ctx, &ctx->dgA, &ctx->gA_cap, opA + nA + (same ? opA : 0)));
+  if (!same) GPR_TRY(ensure_buf(ctx, &ctx->dgB, &ctx->gB_cap, opB + nB));
+  double* A = ctx->dgA;
+  double* nrmA = A + opA;
+  double* B = same ? nrmA + nA : ctx->dgB;
+  double* nrmB = same ? nrmA : B + opB;
+  gram_center_kernel<<<kp.nse * d, 256, 0, ctx->stream>>>(xs, n, d, ctx->dgc);
+  auto prep = [&](const double* src, int cnt, int nblk, double scale, double* out, double* nrm) {
+    const size_t total = (size_t)kp.nse * nblk * S * 64;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    gram_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(src, cnt, d, S, nblk, kp.nse, ctx->dgc,
+                                                      scale, out, nrm);
+  };
+  prep(xs, n, nbA, 2.0, A, nrmA);
+  prep(same ? xs : xps, same ? n : m, nbB, 1.0, B, same ? nullptr : nrmB);
+  LAUNCH_CHECK(ctx);
+  const size_t lds_bytes = sizeof(double) * (KT_LDS + 256 * kp.nse);
+  if (same) {
+    const int nt = (n + KT - 1) / KT;
+    const long long nblk = (long long)nt * (nt + 1) / 2;
+    const int grid = (int)std::min<long long>(nblk, kbuild_grid());
+    kmat_symg_kernel<S><<<grid, 256, lds_bytes, ctx->stream>>>(kp, A, B, nrmA, nbA, n, K,
+                                                               (size_t)ldk, (int)nblk);
+  } else {
+    const int nti = (n + KT - 1) / KT, ntj = (m + KT - 1) / KT;
+    const long long nblk = (long long)nti * ntj;
+    const int grid = (int)std::min<long long>(nblk, kbuild_grid());
+    kmat_crossg_kernel<S><<<grid, 256, lds_bytes, ctx->stream>>>(kp, A, B, nrmA, nrmB, nbA, nbB,
+                                                                 n, m, K, (size_t)ldk, nti,
+                                                                 (int)nblk);
+  }
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int launch_gram_any(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const double* xps,
+                    int m, int same, double* K, int ldk) {
+  switch ((kp.d + 3) / 4) {
+    case 1: return launch_gram<1>(ctx, kp, xs, n, xps, m, same, K, ldk);
+    case 2: return launch_gram<2>(ctx, kp, xs, n, xps, m, same, K, ldk);
+    case 3: return launch_gram<3>(ctx, kp, xs, n, xps, m, same, K, ldk);
+    case 4: return launch_gram<4>(ctx, kp, xs, n, xps, m, same, K, ldk);
+    default: return launch_gram<5>(ctx, kp, xs, n, xps, m, same, K, ldk);
+  }
 }
 
 #define DISPATCH_D(FN, ...)                 \
@@ -574,11 +927,13 @@ int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int 
   if (same) {
     const double el = (double)n * n;
     TimerScope ts(ctx, TC_KBUILD, el * 8.0);  // "flops" slot carries algorithmic bytes
+    if (gram_enabled(kp.d)) return launch_gram_any(ctx, kp, ctx->dxs, n, nullptr, n, 1, dK, ldk);
     DISPATCH_D(launch_sym, ctx, kp, ctx->dxs, n, dK, ldk);
     LAUNCH_CHECK(ctx);
   } else {
     GPR_TRY(scale_inputs(ctx, kp, dXp, m, &ctx->dxps, &ctx->xps_cap));
     TimerScope ts(ctx, TC_OTHER, 0.0);
+    if (gram_enabled(kp.d)) return launch_gram_any(ctx, kp, ctx->dxs, n, ctx->dxps, m, 0, dK, ldk);
     DISPATCH_D(launch_cross, ctx, kp, ctx->dxs, n, ctx->dxps, m, dK, ldk);
     LAUNCH_CHECK(ctx);
   }

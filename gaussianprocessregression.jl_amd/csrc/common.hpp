@@ -90,6 +90,12 @@ struct gpr_ctx {
   size_t xs_cap = 0;
   double* dxps = nullptr;       // per-part scaled second inputs    (nse x d x m)
   size_t xps_cap = 0;
+  double* dgA = nullptr;        // Gram-assembly row operands (MFMA lane order, assembly.hip)
+  size_t gA_cap = 0;
+  double* dgB = nullptr;        // Gram-assembly column operands
+  size_t gB_cap = 0;
+  double* dgc = nullptr;        // Gram-assembly centres (KMAXP x KMAXD)
+  size_t gc_cap = 0;
 
   bool timing = false;
   std::vector<TimedLaunch> pending;

@@ -224,6 +224,9 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dpanel) hipFree(ctx->dpanel);
   if (ctx->dxs) hipFree(ctx->dxs);
   if (ctx->dxps) hipFree(ctx->dxps);
+  if (ctx->dgA) hipFree(ctx->dgA);
+  if (ctx->dgB) hipFree(ctx->dgB);
+  if (ctx->dgc) hipFree(ctx->dgc);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
   return 0;

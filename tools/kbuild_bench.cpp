@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "../include/gpr_hip.h"
 
@@ -12,6 +13,83 @@ __global__ void store16_kernel(double* p, size_t n2) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x)
     reinterpret_cast<d2*>(p)[i] = d2{1.0, 2.0};
+}
+
+__global__ void store8_kernel(double* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = 1.0;
+}
+
+__global__ void store4_kernel(float* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = 1.0f;
+}
+
+// 64 x 64 double tiles in column-major K (ld = N), 512-B column segments, one tile per workgroup
+// iteration: the store shape of the assembly kernels without their math
+__global__ void storetile_kernel(double* K, int N, int ntiles) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int nt = N / 64, l32 = threadIdx.x & 31, cg = threadIdx.x >> 5;
+  for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    const int bi = b % nt, bj = b / nt;
+    double* base = K + (size_t)bi * 64 + 2 * l32 + ((size_t)bj * 64 + cg) * N;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)8 * c * N));
+  }
+}
+
+// TH-row x 64-column tiles, TH/2 lanes of 16 B per column segment
+template <int TH>
+__global__ void storetile_h_kernel(double* K, int N, int ntiles) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  constexpr int LPC = TH / 2;           // lanes per column
+  constexpr int CPI = 256 / LPC;        // columns per instruction
+  const int nt = N / TH, lr = threadIdx.x % LPC, cg = threadIdx.x / LPC;
+  for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    const int bi = b % nt, bj = b / nt;
+    double* base = K + (size_t)bi * TH + 2 * lr + ((size_t)bj * 64 + cg) * N;
+#pragma unroll
+    for (int c = 0; c < 64 / CPI; ++c)
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)CPI * c * N));
+  }
+}
+
+// the symmetric kernel's write shape: upper 64 x 64 tiles in the kernel's triangular order,
+// each written directly and as its mirror
+__global__ void storepair_kernel(double* K, int N, int ntiles) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int l32 = threadIdx.x & 31, cg = threadIdx.x >> 5;
+  for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
+    int bj = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+    while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
+    while (bj * (bj + 1) / 2 > bid) --bj;
+    const int bi = bid - bj * (bj + 1) / 2;
+    double* base = K + (size_t)bi * 64 + 2 * l32 + ((size_t)bj * 64 + cg) * N;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)8 * c * N));
+    if (bi == bj) continue;
+    double* mb = K + (size_t)bj * 64 + 2 * l32 + ((size_t)bi * 64 + cg) * N;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      __builtin_nontemporal_store(d2{3.0, 4.0}, reinterpret_cast<d2*>(mb + (size_t)8 * c * N));
+  }
+}
+
+// one 16-B store per thread, no loop (the blit-kernel shape)
+__global__ void store16flat_kernel(double* p) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  reinterpret_cast<d2*>(p)[blockIdx.x * (size_t)blockDim.x + threadIdx.x] = d2{1.0, 2.0};
+}
+
+// four consecutive 16-B stores per thread per iteration (4 KB contiguous per wave-instruction group)
+__global__ void store16x4_kernel(double* p, size_t n2) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  for (size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) * 4; i < n2; i += (size_t)gridDim.x * blockDim.x * 4) {
+    d2* q = reinterpret_cast<d2*>(p) + i;
+    q[0] = d2{1.0, 2.0}; q[1] = d2{1.0, 2.0}; q[2] = d2{1.0, 2.0}; q[3] = d2{1.0, 2.0};
+  }
 }
 
 __global__ void store16nt_kernel(double* p, size_t n2) {
@@ -41,7 +119,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  {
+  if (!getenv("KB_ONLY")) {
     const size_t bytes = sizeof(double) * (size_t)N * N;
     for (int rep = 0; rep < 4; ++rep) {
       hipEventRecord(e0, s);
@@ -74,9 +152,53 @@ int main(int argc, char** argv) {
       printf("store16 nt grid %d: %.3f ms  %.0f GB/s\n", g, best, bytes / best / 1e6);
     }
   }
+  if (!getenv("KB_ONLY")) {
+    const size_t bytes = sizeof(double) * (size_t)N * N;
+    auto timeit = [&](auto launch, const char* what) {
+      float best = 1e30f;
+      for (int rep = 0; rep < 4; ++rep) {
+        hipEventRecord(e0, s);
+        launch();
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best = ms < best ? ms : best;
+      }
+      printf("%-28s %.3f ms  %.0f GB/s\n", what, best, bytes / best / 1e6);
+    };
+    for (int g : {2048, 16384}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "store8 grid %d", g);
+      timeit([&] { store8_kernel<<<g, 256, 0, s>>>(K, bytes / 8); }, nm);
+      snprintf(nm, sizeof nm, "store4 grid %d", g);
+      timeit([&] { store4_kernel<<<g, 256, 0, s>>>((float*)K, bytes / 4); }, nm);
+      const int ntl = (N / 64) * (N / 64);
+      snprintf(nm, sizeof nm, "storetile grid %d", g);
+      timeit([&] { storetile_kernel<<<g, 256, 0, s>>>(K, N, ntl); }, nm);
+      snprintf(nm, sizeof nm, "storetile h128 grid %d", g);
+      timeit([&] { storetile_h_kernel<128><<<g, 256, 0, s>>>(K, N, ntl / 2); }, nm);
+      snprintf(nm, sizeof nm, "storetile h256 grid %d", g);
+      timeit([&] { storetile_h_kernel<256><<<g, 256, 0, s>>>(K, N, ntl / 4); }, nm);
+      const int ntp = (N / 64) * (N / 64 + 1) / 2;
+      snprintf(nm, sizeof nm, "storepair grid %d", g);
+      timeit([&] { storepair_kernel<<<g, 256, 0, s>>>(K, N, ntp); }, nm);
+      snprintf(nm, sizeof nm, "store16x4 grid %d", g);
+      timeit([&] { store16x4_kernel<<<g, 256, 0, s>>>(K, bytes / 16); }, nm);
+    }
+    timeit([&] { store16flat_kernel<<<(unsigned)(bytes / 16 / 256), 256, 0, s>>>(K); }, "store16flat");
+    {
+      const int ntl = (N / 64) * (N / 64), ntp = (N / 64) * (N / 64 + 1) / 2;
+      timeit([&] { storetile_kernel<<<ntl, 256, 0, s>>>(K, N, ntl); }, "storetile 1 tile/WG");
+      timeit([&] { storetile_h_kernel<128><<<ntl / 2, 256, 0, s>>>(K, N, ntl / 2); }, "storetile h128 1 tile/WG");
+      timeit([&] { storepair_kernel<<<ntp, 256, 0, s>>>(K, N, ntp); }, "storepair 1 tile/WG");
+      timeit([&] { store16_kernel<<<(unsigned)(bytes / 16 / 256 / 16), 256, 0, s>>>(K, bytes / 16); }, "store16 16/thread grid-stride");
+    }
+  }
   struct Cfg { const char* name; std::vector<int> kinds; };
   std::vector<Cfg> cfgs = {{"SE", {GPR_SE}}, {"SE+WN", {GPR_SE, GPR_WN}}, {"SE+SE+WN", {GPR_SE, GPR_SE, GPR_WN}}};
+  const char* only = getenv("KB_ONLY");
   for (auto& c : cfgs) {
+    if (only && strcmp(only, c.name) != 0) continue;
     std::vector<double> hp;
     for (int k : c.kinds) {
       if (k == GPR_SE) { hp.push_back(1.0); for (int t = 0; t < d; ++t) hp.push_back(l); }

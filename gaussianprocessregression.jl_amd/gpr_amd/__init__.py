@@ -39,4 +39,26 @@ from .core import (
     update_cache_,
 )
 
+from .train import (
+    BFGS,
+    LBFGS,
+    BFGSQuad,
+    BFGSQuadCache,
+    ConjugateGradient,
+    NelderMead,
+    NewtonTrustRegion,
+    Options,
+    OptimResult,
+    bfgs_hessian,
+    bfgs_quad,
+    bfgs_quad_,
+    g_converged,
+    hessian_fd,
+    hessian_fd_,
+    init_params,
+    minimizer,
+    train,
+    update_sample_,
+)
+
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -233,6 +233,11 @@ class GPRModel:
             self._dy = self.ctx.colmajor(self.y)
         return self._dy
 
+    def add_to_y(self, dy):
+        """md.y .+= dy (src/update_model.jl:43); the device copy is refreshed on next use."""
+        self.y = self.y + np.asarray(dy, dtype=np.float64)
+        self._dy = None
+
     def dsample(self) -> torch.Tensor:
         """get_sample(md) on the device (src/models.jl:39-45)."""
         y = self.dy()

@@ -4,9 +4,12 @@
 Workload (BASELINE config 3, the config the headline metric is quoted on): composed kernel
 SquaredExp + SquaredExp + WhiteNoise (the parity-pinned stand-in for "SE + periodic": the
 reference has no periodic kernel), N = 32768 training points, d = 8, fp64.
-One step = one GP job on each GPU:
+One step = one GP job on each GPU, the reference's predict(md, xp; diagonal_var=true) from
+scratch (src/predict.jl:14-71: update_cache! = K, cholesky!, ldiv! against y; then predict!)
+as ONE call, gpr_fit_predict:
     fit      : K-assembly (N x N) + in-place blocked POTRF + POTRS (alpha = K^{-1} y)
     posterior: cross kernel (N x np) + mean + diagonal variance for np = 8192 test points
+(GPR_FUSED_RHS=1/2 solves [K(x, xp) | y] inside the factorisation instead: measured slower.)
 Synthetic data: x ~ U[0,1)^(d x N) seed 0 (+rank), y = sin(sum x)^2, test points
 seed 1 (+rank); hp sigma = 1, l = 3 sqrt(8/d), sigma_n = 0.1.  All inputs are resident in
 HBM before the timed region.
@@ -175,23 +178,24 @@ def main():
     alpha = ctx.empty(N)
     mu = ctx.empty(NP)
     var = ctx.empty(NP)
-    work = ctx.empty(NP, N)
+    work = ctx.empty(NP + 1, N)   # [K(x, xp) | y], column-major N x (np + 1)
     info = ctypes.c_int(0)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
-    def fit():
-        rc = lib.gpr_fit(ctx.h, karr, len(kinds), hpp, d, P(dx), N, P(dy), 1, N, 1e-8, P(K), N,
-                         P(alpha), ctypes.byref(info))
+    def fit_predict():
+        rc = lib.gpr_fit_predict(ctx.h, karr, len(kinds), hpp, d, P(dx), N, P(dy), 1, N, 1e-8,
+                                 P(K), N, P(alpha), P(dxp), NP, 1, P(mu), P(var), NP, P(work),
+                                 ctypes.byref(info))
         if rc != 0:
-            raise RuntimeError(f"gpr_fit rc={rc} info={info.value}: {lib.gpr_last_error(ctx.h)}")
+            raise RuntimeError(f"gpr_fit_predict rc={rc} info={info.value}: "
+                               f"{lib.gpr_last_error(ctx.h)}")
 
     def posterior():
         ctx.check(lib.gpr_predict(ctx.h, karr, len(kinds), hpp, d, P(dx), N, P(K), N, P(alpha), 1,
                                   P(dxp), NP, 1, 1e-8, P(mu), P(var), NP, P(work)), "gpr_predict")
 
     def step():
-        fit()
-        posterior()
+        fit_predict()
 
     def barrier():
         if world > 1:
@@ -216,12 +220,13 @@ def main():
         dt = float(tt.item())
     ok = bool(torch.isfinite(mu).all().item() and torch.isfinite(var).all().item())
 
-    # ---- instrumented step (HIP events on the context stream) --------------------------
+    # ---- instrumented steps (HIP events on the context stream) --------------------------
+    # (a) the unfused reference order (gpr_kernel, gpr_potrf_upper, gpr_potrs_upper,
+    #     gpr_predict) for a per-stage breakdown; (b) the fused step with kernel-level timing
+    #     classes (K-build bandwidth, pipelined-GEMM roofline).
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     stg = {}
     with torch.cuda.stream(ctx.stream):
-        lib.gpr_timing_reset(ctx.h)
-        lib.gpr_timing_enable(ctx.h, 1)
         e = [ev() for _ in range(5)]
         e[0].record(ctx.stream)
         kinds_k = (ctypes.c_int * len(kinds))(*kinds)
@@ -236,10 +241,19 @@ def main():
         posterior()
         e[4].record(ctx.stream)
         ctx.sync()
+        f0, f1 = ev(), ev()
+        lib.gpr_timing_reset(ctx.h)
+        lib.gpr_timing_enable(ctx.h, 1)
+        f0.record(ctx.stream)
+        fit_predict()
+        f1.record(ctx.stream)
+        ctx.sync()
         lib.gpr_timing_enable(ctx.h, 0)
+    fused_ms = f0.elapsed_time(f1)
     names = ["kbuild", "potrf", "potrs", "posterior"]
     for i, nm in enumerate(names):
         stg[nm] = e[i].elapsed_time(e[i + 1])
+    unfused_ms = sum(stg.values())
     cls = {}
     for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other", "gemm_pipe"]):
         ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
@@ -276,7 +290,9 @@ def main():
             "kbuild_hbm_frac": kbuild_gbs / HBM_PEAK_GBS,
             "potrf_TFLOPs": potrf_tf,
             "potrf_mfma_frac": potrf_tf / FP64_MFMA_PEAK,
-            "stage_ms": stg,
+            "stage_ms_unfused": stg,
+            "unfused_job_ms": unfused_ms,
+            "fused_job_ms": fused_ms,
             "syrk_TFLOPs": cls["syrk"][2] / (cls["syrk"][0] * 1e-3) / 1e12 if cls["syrk"][0] else None,
             "roofline": {
                 "kernel": " + ".join(DOMINANT_KERNELS),

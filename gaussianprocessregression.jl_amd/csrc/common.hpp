@@ -53,6 +53,11 @@ struct gpr_ctx {
   int inner_la = 0;               // split the panel inner update (GPR_INNER_LA=1; no gain measured)
   hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
   hipStream_t smain = nullptr;    // big trailing updates: CU mask = all but the reserved CUs
+  hipStream_t srhs = nullptr;     // right-hand-side solves fused into the factorisation
+  hipStream_t ssq = nullptr;      // square inverses of finished outer panels (fused solves)
+  // gpr_fit_predict: 0 = factor, then solve (default); 1 / 2 = solve inside the factorisation
+  // on its own stream / on the main stream (GPR_FUSED_RHS; measured slower at C3: 347 vs 334 ms)
+  int fused_rhs = 0;
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   std::vector<hipEvent_t> sync_events;
@@ -90,6 +95,10 @@ struct gpr_ctx {
   size_t xs_cap = 0;
   double* dxps = nullptr;       // per-part scaled second inputs    (nse x d x m)
   size_t xps_cap = 0;
+  double* dscr_wt = nullptr;     // gpr_fit_predict: K^{-1} y when the caller passes no alpha
+  size_t scr_wt_cap = 0;
+  double* dpanel_rhs = nullptr;  // solved outer panel of the fused right-hand sides
+  size_t panel_rhs_cap = 0;
   double* dgA = nullptr;        // Gram-assembly row operands (MFMA lane order, assembly.hip)
   size_t gA_cap = 0;
   double* dgB = nullptr;        // Gram-assembly column operands
@@ -171,9 +180,22 @@ int launch_scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n
 int launch_pair(gpr_ctx* ctx, int mode, int d, const double* xa, int na, const double* xb, int nb,
                 double s2, double* out, size_t sa, size_t sb);
 int launch_set_identity(gpr_ctx* ctx, double* A, int n, int lda);
-int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info);
+// Right-hand sides solved during the factorisation: B <- U^{-T} B (outer panel s of B is
+// solved as soon as panel s of U is final, on ctx->srhs beside the trailing updates).
+// lower_rhs: B is lower triangular (identity), outer block s touches columns < (s+1) nb2.
+struct RhsSpec {
+  double* B;
+  int nrhs;
+  int ldb;
+  int lower_rhs;
+};
+int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
+               const RhsSpec* rhs = nullptr);
 int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs);
-int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
-               int ldb);
+// norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream
+int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm);
+// forward = false: only the backward sweep U x = B (B already holds U^{-T} b)
+int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs, int ldb,
+               bool forward = true);

@@ -147,10 +147,13 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   int prio_lo = 0, prio_hi = 0;
   hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->srhs, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->ssq, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return GPR_E_HIP;
   }
+  if (const char* e = getenv("GPR_FUSED_RHS")) ctx->fused_rhs = atoi(e);
   if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
   if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
   if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);
@@ -210,6 +213,10 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   for (auto e : ctx->sync_events) hipEventDestroy(e);
   if (ctx->stream2) hipStreamDestroy(ctx->stream2);
   if (ctx->stream3) hipStreamDestroy(ctx->stream3);
+  if (ctx->srhs) hipStreamDestroy(ctx->srhs);
+  if (ctx->ssq) hipStreamDestroy(ctx->ssq);
+  if (ctx->dpanel_rhs) hipFree(ctx->dpanel_rhs);
+  if (ctx->dscr_wt) hipFree(ctx->dscr_wt);
   if (ctx->sdiag) hipStreamDestroy(ctx->sdiag);
   if (ctx->smain) hipStreamDestroy(ctx->smain);
   if (ctx->winv) hipFree(ctx->winv);

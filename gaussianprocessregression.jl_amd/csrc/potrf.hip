@@ -1166,10 +1166,11 @@ __global__ __launch_bounds__(SW_THREADS) void trsv_bwd_sweep_kernel(
 
 template <int NR>
 static void launch_sweeps(gpr_ctx* ctx, const double* U, size_t ldu, int n, double* B,
-                          size_t ldb, int* sync) {
+                          size_t ldb, int* sync, bool forward) {
   const int nblk = (n + SW_NB - 1) / SW_NB;
-  trsv_fwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
-                                                                  ctx->dtrsv, sync);
+  if (forward)
+    trsv_fwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
+                                                                    ctx->dtrsv, sync);
   trsv_bwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
                                                                   ctx->dtrsv, sync + 2);
 }
@@ -1319,12 +1320,12 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
 // inverses W_i (final), so the workgroups are independent (no hand-offs).
 //   X_cc = W_c,  X_ic = -W_i sum_{t=i+1..c} U(i, t) X_tc   (i = c-1 .. 0)
 __global__ __launch_bounds__(256, 1) void sqinv_kernel(const double* __restrict__ U, size_t ldu,
-                                                       int n, int nb2,
+                                                       int n, int nb2, int p0,
                                                        const double* __restrict__ winv,
                                                        double* __restrict__ sqinv) {
   constexpr int NB = 128;
   __shared__ double glds[2 * 4096];
-  const int p = blockIdx.x, c = blockIdx.y;
+  const int p = p0 + blockIdx.x, c = blockIdx.y;
   const int k = p * nb2, kw = min(nb2, n - k);
   if (c * NB >= kw) return;
   auto blk = [&](int i, int j) { return U + (size_t)(k + i * NB) + (size_t)(k + j * NB) * ldu; };
@@ -1438,6 +1439,35 @@ int trsm_panel(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
   return 0;
 }
 
+// Outer panel k of a right-hand-side block on the square inverse (the loop body of
+// trsm_ut_sq): X_k = U_sq_k^{-T} B_k (one GEMM, K range cut at each tile's diagonal), the update
+// B_rest -= U_k,rest^T X_k (K = nb2), X_k copied back.  Everything on ctx->ls.
+int rhs_panel_step(gpr_ctx* ctx, const double* dU, int n, int ldu, const RhsSpec& r, int k,
+                   int nb2, double* panelbuf) {
+  const int kw = std::min(nb2, n - k), kend = k + kw;
+  const int nc = r.lower_rhs ? std::min(r.nrhs, kend) : r.nrhs;
+  GemmArgs g{};
+  g.P = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2; g.ldp = kw;
+  g.Q = r.B + k; g.ldq = r.ldb;
+  g.C = panelbuf; g.ldc = kw;
+  g.M = kw; g.N = nc; g.K = kw;
+  g.alpha = 1.0; g.beta = 0.0;
+  g.kend_from_m = 1;
+  g.info = ctx->dinfo;
+  GPR_TRY(launch_gemm_tn(ctx, g, TC_TRSM_GEMM));
+  if (kend < n) {
+    GemmArgs b{};
+    b.P = dU + k + (size_t)kend * ldu; b.ldp = ldu;
+    b.Q = panelbuf; b.ldq = kw;
+    b.C = r.B + kend; b.ldc = r.ldb;
+    b.M = n - kend; b.N = nc; b.K = kw;
+    b.alpha = -1.0; b.beta = 1.0;
+    b.info = ctx->dinfo;
+    GPR_TRY(launch_gemm_tn(ctx, b, TC_TRSM_GEMM));
+  }
+  return launch_copy_panel(ctx, panelbuf, kw, r.B + k, r.ldb, kw, nc);
+}
+
 }  // namespace
 
 // Two-level right-looking upper Cholesky with depth-1 lookahead.
@@ -1445,11 +1475,21 @@ int trsm_panel(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
 //   stream2 (panel):  wait b_{s-1}; a_s = update of rows P_{s+1} by P_s; factor P_{s+1}
 //   stream  (main):   wait panel_s; b_s = SYRK of rows/cols >= (s+2)*nb2 by P_s
 // so the latency-bound diag/TRSM chain of panel s+1 overlaps the big SYRK b_s.
-int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
+//   srhs (rhs, optional): wait panel_s final; U_sq_s^{-1}; solve outer block s of B and update
+//                         the rows below (rhs_panel_step) -- the triangular solve rides in the
+//                         bubbles of the lookahead chain instead of running after the factor.
+int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpec* rhs) {
   const int nb = ctx->nb;
   const int nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
   ctx->fac_valid = false;
+  ctx->sqinv_nb2 = 0;
   GPR_TRY(ensure_winv(ctx, n, nb));
+  if (rhs && (nb != 128 || nb2 > 2048 || !ctx->srhs || rhs->nrhs <= 0)) rhs = nullptr;
+  if (rhs) {
+    GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap,
+                       (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));
+    GPR_TRY(ensure_buf(ctx, &ctx->dpanel_rhs, &ctx->panel_rhs_cap, (size_t)nb2 * rhs->nrhs));
+  }
   hipStream_t user = ctx->stream;
   hipStream_t s0 = ctx->smain ? ctx->smain : ctx->stream, s1 = ctx->stream2;
   HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), user));
@@ -1459,18 +1499,48 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
   HIP_TRY(ctx, hipEventRecord(e0, user));
   HIP_TRY(ctx, hipStreamWaitEvent(s1, e0, 0));
   if (s0 != user) HIP_TRY(ctx, hipStreamWaitEvent(s0, e0, 0));
+  // fused_rhs 1: right-hand sides on their own stream (srhs); 2: on the main stream after each
+  // trailing SYRK (serialised with the big updates, overlapping only the panel chain)
+  hipStream_t sr = !rhs ? nullptr : (ctx->fused_rhs == 2 ? s0 : ctx->srhs);
+  if (sr && sr != s0) HIP_TRY(ctx, hipStreamWaitEvent(sr, e0, 0));
   ctx->ls = s1;
   const bool sqp = ctx->panel_sq && nb == 128 && nb2 <= 2048;
   auto panel = [&](int k, int kw) {
     return sqp ? factor_panel_sq(ctx, dA, n, lda, k, kw) : factor_panel(ctx, dA, n, lda, k, kw);
   };
-  ctx->sqinv_nb2 = 0;
+  // outer block k of the right-hand sides once panel k of U is final (event ev_final)
+  // U_sq^{-1} of outer panel k on ssq once the panel is final (off the solve's own chain);
+  // the square path wrote it already
+  auto sq_inverse = [&](int k, hipEvent_t ev_final) -> hipEvent_t {
+    if (!sr || sqp) return ev_final;
+    if (hipStreamWaitEvent(ctx->ssq, ev_final, 0) != hipSuccess) return nullptr;
+    ctx->ls = ctx->ssq;
+    {
+      TimerScope ts(ctx, TC_OTHER, 0.0);
+      sqinv_kernel<<<dim3(1, nb2 / nb), 256, 0, ctx->ssq>>>(dA, (size_t)lda, n, nb2, k / nb2,
+                                                            ctx->winv, ctx->dsqinv);
+    }
+    hipEvent_t es = sync_event(ctx, ev++);
+    if (hipEventRecord(es, ctx->ssq) != hipSuccess) return nullptr;
+    return es;
+  };
+  // outer block k of the right-hand sides once U_sq^{-1} of panel k exists (event ev_sq)
+  auto rhs_step = [&](int k, hipEvent_t ev_sq) -> int {
+    if (!sr) return 0;
+    ctx->ls = sr;
+    HIP_TRY(ctx, hipStreamWaitEvent(sr, ev_sq, 0));
+    return rhs_panel_step(ctx, dA, n, lda, *rhs, k, nb2, ctx->dpanel_rhs);
+  };
   int rc = panel(0, std::min(nb2, n));
   hipEvent_t ev_p = sync_event(ctx, ev++);
   hipEvent_t ev_b = nullptr;
   if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
   for (int k = 0; !rc && k + nb2 < n; k += nb2) {
     const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
+    // ---- square inverse of panel s, then (srhs mode) outer block s of B
+    hipEvent_t ev_sq = sq_inverse(k, ev_p);
+    if (!ev_sq) { rc = GPR_E_HIP; break; }
+    if (sr != s0 && (rc = rhs_step(k, ev_sq))) break;
     // ---- panel stream: a_s (rows P_{s+1} by P_s), then factor panel s+1
     ctx->ls = s1;
     if (ev_b && hipStreamWaitEvent(s1, ev_b, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
@@ -1518,7 +1588,18 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
     }
     ev_b = sync_event(ctx, ev++);
     if (hipEventRecord(ev_b, s0) != hipSuccess) { rc = GPR_E_HIP; break; }
+    if (sr == s0 && (rc = rhs_step(k, ev_sq))) break;  // after b_s, beside the panel chain
     ev_p = ev_p_next;
+  }
+  if (!rc && sr) {  // the last outer block
+    const int kl = ((n - 1) / nb2) * nb2;
+    hipEvent_t ev_sq = sq_inverse(kl, ev_p);
+    rc = ev_sq ? rhs_step(kl, ev_sq) : GPR_E_HIP;
+  }
+  if (sr && sr != s0) {
+    hipEvent_t er = sync_event(ctx, ev++);
+    HIP_TRY(ctx, hipEventRecord(er, sr));
+    HIP_TRY(ctx, hipStreamWaitEvent(user, er, 0));
   }
   ctx->ls = user;
   hipEvent_t ej = sync_event(ctx, ev++);  // join the panel and main streams into the user's
@@ -1534,7 +1615,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info) {
   HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, user));
   HIP_TRY(ctx, hipStreamSynchronize(user));
   if (info) *info = hinfo;
-  if (hinfo == 0 && sqp) {
+  if (hinfo == 0 && (sqp || rhs)) {
     ctx->sqinv_nb2 = nb2;
     ctx->sq_ptr = dA;
     ctx->sq_n = n;
@@ -1579,8 +1660,8 @@ int ensure_sq_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
   GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap, (size_t)np * nb2 * nb2));
   {
     TimerScope ts(ctx, TC_OTHER, 0.0);
-    sqinv_kernel<<<dim3(np, nb2 / NB), 256, 0, ctx->stream>>>(dU, (size_t)ldu, n, nb2, ctx->winv,
-                                                              ctx->dsqinv);
+    sqinv_kernel<<<dim3(np, nb2 / NB), 256, 0, ctx->stream>>>(dU, (size_t)ldu, n, nb2, 0,
+                                                              ctx->winv, ctx->dsqinv);
     LAUNCH_CHECK(ctx);
   }
   ctx->sqinv_nb2 = nb2;
@@ -1637,6 +1718,14 @@ static int trsm_ut_sq(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB
     colnorm_sub_kernel<<<(nrhs + 3) / 4, 256, 0, s0>>>(dB, (size_t)ldb, n, nrhs, norm_out);
     LAUNCH_CHECK(ctx);
   }
+  return 0;
+}
+
+int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm) {
+  if (ncols <= 0) return 0;
+  TimerScope ts(ctx, TC_OTHER, 0.0);
+  colnorm_sub_kernel<<<(ncols + 3) / 4, 256, 0, ctx->stream>>>(dB, (size_t)ldb, n, ncols, norm);
+  LAUNCH_CHECK(ctx);
   return 0;
 }
 
@@ -1700,7 +1789,8 @@ int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int
 }
 
 // B <- K^{-1} B with small nrhs (dpotrs): blocked forward U^T z = b, backward U x = z.
-int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs, int ldb) {
+int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs, int ldb,
+               bool forward) {
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   const int nb = ctx->nb;
   const int nblk = (n + nb - 1) / nb;
@@ -1713,9 +1803,9 @@ int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
       HIP_TRY(ctx, hipMemsetAsync(sync, 0, 4 * sizeof(int), ctx->stream));
       TimerScope ts(ctx, TC_OTHER, 0.0);
       if (nc == 1)
-        launch_sweeps<1>(ctx, dU, ldu, n, B, ldb, sync);
+        launch_sweeps<1>(ctx, dU, ldu, n, B, ldb, sync, forward);
       else
-        launch_sweeps<2>(ctx, dU, ldu, n, B, ldb, sync);
+        launch_sweeps<2>(ctx, dU, ldu, n, B, ldb, sync, forward);
       LAUNCH_CHECK(ctx);
     }
     return 0;
@@ -1724,7 +1814,7 @@ int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
     const int nc = std::min(RHS_CHUNK, nrhs - c0);
     double* B = dB + (size_t)c0 * ldb;
     // forward
-    for (int b = 0; b < nblk; ++b) {
+    for (int b = 0; forward && b < nblk; ++b) {
       const int k = b * nb, kb = std::min(nb, n - k);
       const double* wk = ctx->winv + (size_t)b * nb * nb;
       trsv_diag_kernel<<<1, 256, 0, ctx->stream>>>(wk, nb, kb, B + k, (size_t)ldb, nc, 1);

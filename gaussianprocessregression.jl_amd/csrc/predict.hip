@@ -153,6 +153,76 @@ int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d
   return launch_mirror_upper(ctx, dvar, m, ldv);
 }
 
+int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                    const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
+                    double* dK, int ldk, double* dalpha, const double* dXp, int m, int mode,
+                    double* dmu, double* dvar, int ldv, double* dwork, int* info) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (n <= 0 || m <= 0 || ldk < n || nrhs <= 0 || ldy < n || !dX || !dy || !dK || !dXp || !dmu)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  if (mode != GPR_PREDICT_MEAN && !dvar) return set_err(ctx, GPR_E_ARG, "dvar is NULL");
+  if (mode == GPR_PREDICT_FULL && ldv < m) return set_err(ctx, GPR_E_ARG, "ldv < m");
+  if (mode == GPR_PREDICT_MEAN || !ctx->fused_rhs) {
+    // nothing to fuse for the mean alone (mu = K(xp, x) alpha); or the unfused reference order
+    double* wt = dalpha;
+    if (!wt) {
+      GPR_TRY(ensure_buf(ctx, &ctx->dscr_wt, &ctx->scr_wt_cap, (size_t)n * nrhs));
+      wt = ctx->dscr_wt;
+    }
+    int hinfo = 0;
+    const int rc = gpr_fit(ctx, kinds, nk, hp, d, dX, n, dy, nrhs, ldy, eps, dK, ldk, wt, &hinfo);
+    if (info) *info = hinfo;
+    if (rc) return rc;
+    return gpr_predict(ctx, kinds, nk, hp, d, dX, n, dK, ldk, wt, nrhs, dXp, m, mode, eps, dmu,
+                       dvar, ldv, dwork);
+  }
+  // W = [K(x, xp) | y] (n x (m + nrhs)); POTRF solves W <- U^{-T} W in its lookahead bubbles:
+  // V = U^{-T} K(x, xp) and z = U^{-T} y, then mu = V^T z (= K(xp, x) K^{-1} y) and
+  // var = prior - ||V_j||^2; alpha = U^{-1} z by the backward sweep alone.
+  double* W = dwork;
+  if (!W) {
+    GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)n * (m + nrhs)));
+    W = ctx->dbig2;
+  }
+  double* Z = W + (size_t)n * m;
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, W, n));
+  HIP_TRY(ctx, hipMemcpy2DAsync(Z, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
+                                (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
+  RhsSpec rhs{W, m + nrhs, n, 0};
+  int hinfo = 0;
+  GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
+  if (info) *info = hinfo;
+  if (hinfo != 0) return hinfo;
+  {
+    TimerScope ts(ctx, TC_OTHER, 0.0);
+    colgemv_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(W, (size_t)n, n, m, Z, (size_t)n, nrhs,
+                                                         dmu, (size_t)m);
+    LAUNCH_CHECK(ctx);
+  }
+  if (dalpha) {
+    HIP_TRY(ctx, hipMemcpy2DAsync(dalpha, (size_t)n * sizeof(double), Z, (size_t)n * sizeof(double),
+                                  (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice,
+                                  ctx->stream));
+    GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n, /*forward=*/false));
+  }
+  if (mode == GPR_PREDICT_DIAG) {
+    GPR_TRY(launch_fill(ctx, dvar, (size_t)m, diag_prior(kinds, nk, hp, d)));
+    return launch_colnorm_sub(ctx, W, n, n, m, dvar);
+  }
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dXp, m, nullptr, m, 1, dvar, ldv));
+  GemmArgs g{};
+  g.P = W; g.ldp = n;
+  g.Q = W; g.ldq = n;
+  g.C = dvar; g.ldc = ldv;
+  g.M = m; g.N = m; g.K = n;
+  g.alpha = -1.0; g.beta = 1.0;
+  g.upper = 1;
+  GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+  return launch_mirror_upper(ctx, dvar, m, ldv);
+}
+
 int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                       const double* dX, int ns, const double* dXe, int ne, const double* dXq,
                       int nq, int part, double* dA, double* dB, double* dC) {

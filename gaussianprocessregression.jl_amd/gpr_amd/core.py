@@ -502,13 +502,31 @@ def predict(md: GPRModel, xp, diagonal_var: bool = False, eps: float = EPS_DEFAU
     if isinstance(xp, Cmap):
         return _split_predict(md, xp, eps=eps, var_range=var_range)
     ctx = md.ctx
-    m = np.asarray(xp).shape[-1]
-    pc = GPRPredictCache(md, m)
-    _update_predict_cache(pc, md, eps)
+    pc = GPRPredictCache(md, 0)
+    dxp = ctx.colmajor(xp)
+    m = dxp.shape[0]
     mu = ctx.empty(pc.nrhs, m) if pc.nrhs > 1 else ctx.empty(m)
     Sigma = ctx.empty(m) if diagonal_var else ctx.empty(m, m)
-    predict_(mu, Sigma, md, xp, pc, diagonal_var, eps=eps)
+    _fit_predict(md, dxp, m, pc, mu, Sigma, diagonal_var, eps)
     return ctx.host(mu), ctx.host(Sigma)
+
+
+def _fit_predict(md: GPRModel, dxp, m: int, pc: GPRPredictCache, mu, Sigma, diagonal_var: bool,
+                 eps: float = EPS_DEFAULT):
+    """update_cache!(pc, md) + predict!(mu, Sigma, md, xp, pc) (src/predict.jl:29-71) as ONE
+    device call: the triangular solve of [K(x, xp) | y] runs inside the factorisation
+    (gpr_fit_predict); pc.Kxx receives U (lower triangle keeps K), pc.wt = K^{-1} y."""
+    ctx = md.ctx
+    kinds, nk = _kinds_arr(md.covar)
+    hpa, hpp = _hp_arr(md.params)
+    mode = _lib.GPR_PREDICT_DIAG if diagonal_var else _lib.GPR_PREDICT_FULL
+    info = ctypes.c_int(0)
+    rc = lib.gpr_fit_predict(ctx.h, kinds, nk, hpp, md.d, _ptr(md.dx()), md.n, _ptr(md.dy()),
+                             pc.nrhs, md.n, eps, _ptr(pc.Kxx), md.n, _ptr(pc.wt), _ptr(dxp), m,
+                             mode, _ptr(mu), _ptr(Sigma), m, None, ctypes.byref(info))
+    if info.value != 0:
+        raise PosDefException(info.value)
+    ctx.check(rc, "gpr_fit_predict")
 
 
 # =========================================================================================

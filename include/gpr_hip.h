@@ -153,6 +153,19 @@ int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d
                 int nrhs, const double* dXp, int m, int mode, double eps, double* dmu,
                 double* dvar, int ldv, double* dwork);
 
+/* ---- a5/a6/a10/a11 fused: predict(md, xp; diagonal_var) from scratch ---------------- */
+/* The reference's predict (src/predict.jl:14-25 -> update_cache!(pc, md) :29-34 = K, cholesky!,
+ * ldiv!(wt, kchol, md.y), then predict! :36-71) in one call: K(x, x) into dK (upper
+ * overwritten by U, lower keeps K, as gpr_fit), posterior mean/variance at m test points as
+ * gpr_predict.  With mode DIAG/FULL the triangular solve of [K(x, xp) | y] runs inside the
+ * factorisation (outer block s solved once panel s of U is final), mu = V^T z with
+ * V = U^{-T} K(x, xp), z = U^{-T} y; dalpha (optional, n x nrhs) = K^{-1} y.  dwork: optional
+ * n*(m+nrhs) doubles.  Returns >0 (LAPACK info) for a non-PD K. */
+int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                    const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
+                    double* dK, int ldk, double* dalpha, const double* dXp, int m, int mode,
+                    double* dmu, double* dvar, int ldv, double* dwork, int* info);
+
 /* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
 /* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).
  * dmu: ne x nq column-major (index e + q*ne, src/split_predict.jl:10-19).

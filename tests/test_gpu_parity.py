@@ -523,3 +523,92 @@ def test_split_predict_full_var_range_and_rows():
     assert np.all(m2[:4] == 0) and np.all(m2[9:] == 0)
     np.testing.assert_allclose(v2[4 * q:9 * q], var_o[4 * q:9 * q], rtol=1e-8, atol=1e-8 * O.diag_prior(kinds, hp, dim))
     assert np.all(v2[:4 * q] == 0) and np.all(v2[9 * q:] == 0)
+
+
+# ---------------------------------------------------------------------------------------
+# a5/a6/a10/a11 fused: predict from scratch with the solve inside the factorisation
+# ---------------------------------------------------------------------------------------
+def _fit_predict_dev(ctx, kinds, hp, x, y, xp, mode, nb2=None):
+    if nb2:
+        assert G._lib.lib.gpr_set_outer_block(ctx.h, nb2) == 0
+    d, n = x.shape
+    m = xp.shape[1]
+    y2 = y if y.ndim == 2 else y[:, None]
+    nrhs = y2.shape[1]
+    dx, dy, dxp = ctx.colmajor(x), ctx.colmajor(y2), ctx.colmajor(xp)
+    K = ctx.empty(n, n)
+    alpha = ctx.empty(nrhs, n)
+    mu = ctx.empty(nrhs, m)
+    var = ctx.empty(m) if mode == G.GPR_PREDICT_DIAG else ctx.empty(m, m)
+    karr = (ctypes.c_int * len(kinds))(*[1 if k == SE else 2 for k in kinds])
+    hpa = np.asarray(hp, dtype=np.float64)
+    info = ctypes.c_int(-1)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rc = G._lib.lib.gpr_fit_predict(ctx.h, karr, len(kinds),
+                                    hpa.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), d, P(dx),
+                                    n, P(dy), nrhs, n, 1e-8, P(K), n, P(alpha), P(dxp), m, mode,
+                                    P(mu), P(var), m, None, ctypes.byref(info))
+    assert rc == 0 and info.value == 0, G._lib.lib.gpr_last_error(ctx.h)
+    return ctx.host(K), ctx.host(alpha), ctx.host(mu), ctx.host(var)
+
+
+@pytest.mark.parametrize("fused", ["1", "2", "0"])
+@pytest.mark.parametrize("name,n,npred,dim,nb2", [
+    ("SE+WN", 300, 77, 3, None), ("SE+SE+WN", 1300, 200, 8, 256), ("SE+WN", 1025, 64, 2, 1024),
+    ("SE+WN", 2600, 500, 5, 1024), ("SE+SE", 700, 1000, 4, 512)])
+def test_fit_predict_fused_vs_oracle(name, n, npred, dim, nb2, fused, monkeypatch):
+    """gpr_fit_predict = predict(md, xp; diagonal_var) from scratch (src/predict.jl:14-71):
+    U in the upper triangle (lower keeps K), alpha, mean and variance vs the oracle, across
+    outer-panel boundaries (the solve rides inside the factorisation) and ragged panels;
+    fused=0 is the unfused reference order (gpr_fit + gpr_predict)."""
+    monkeypatch.setenv("GPR_FUSED_RHS", fused)
+    kinds = KSETS[name]
+    x, y, xp = O.synthetic(dim, n, npred, seed_train=n, seed_test=npred)
+    hp = O.default_hp(kinds, dim, noise=0.05)
+    ctx = G.Context(0)
+    Kd, alpha, mu, var = _fit_predict_dev(ctx, kinds, hp, x, y, xp, G.GPR_PREDICT_DIAG, nb2)
+    K = O.kernel(kinds, hp, x)
+    U = sla.cholesky(K, lower=False)
+    # the lower triangle keeps K; the upper holds the factor of exactly that K
+    np.testing.assert_allclose(np.tril(Kd, -1), np.tril(K, -1), rtol=1e-13, atol=1e-15)
+    Kdev = np.tril(Kd) + np.tril(Kd, -1).T
+    np.fill_diagonal(Kdev, np.diag(K))
+    assert relnorm(np.triu(Kd), sla.cholesky(Kdev, lower=False)) < 1e-11
+    np.testing.assert_allclose(alpha.ravel(), O.cho_solve_upper(U, y), rtol=1e-8,
+                               atol=1e-10 * np.abs(O.cho_solve_upper(U, y)).max())
+    mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+    vtol = 1e-8 * O.diag_prior(kinds, hp, dim)
+    np.testing.assert_allclose(mu.ravel(), mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=vtol)
+    if n <= 1300:
+        _, _, mu2, S = _fit_predict_dev(ctx, kinds, hp, x, y, xp, G.GPR_PREDICT_FULL, nb2)
+        _, S_o = O.predict(kinds, hp, x, y, xp, diagonal_var=False)
+        np.testing.assert_allclose(mu2.ravel(), mu_o, rtol=1e-8, atol=1e-10)
+        np.testing.assert_allclose(S, S_o, rtol=1e-8, atol=vtol)
+
+
+def test_fit_predict_multi_output_and_reuse():
+    """Multi-column y (md.y N x ne, src/predict.jl:32 solves against all columns); the factor
+    and square inverses left by the fused call serve later solves on the same context."""
+    kinds = KSETS["SE+WN"]
+    dim, n, m = 4, 1100, 150
+    x, _, xp = O.synthetic(dim, n, m, seed_train=5, seed_test=6)
+    Y = np.stack([np.sin(x.sum(0)), np.cos(x[0]) + x[1]], axis=1)
+    hp = O.default_hp(kinds, dim, noise=0.05)
+    ctx = G.Context(0)
+    assert G._lib.lib.gpr_set_outer_block(ctx.h, 512) == 0
+    Kd, alpha, mu, var = _fit_predict_dev(ctx, kinds, hp, x, Y, xp, G.GPR_PREDICT_DIAG)
+    K = O.kernel(kinds, hp, x)
+    U = sla.cholesky(K, lower=False)
+    Kxp = O.kernel(kinds, hp, xp, x)
+    for c in range(2):
+        a_o = O.cho_solve_upper(U, Y[:, c])
+        np.testing.assert_allclose(alpha[:, c], a_o, rtol=1e-8, atol=1e-10 * np.abs(a_o).max())
+        np.testing.assert_allclose(mu[:, c], Kxp @ a_o, rtol=1e-8, atol=1e-10)
+    # reuse: a TRSM against the fused factor on the same context
+    B = np.random.default_rng(1).random((n, 5))
+    dB = ctx.colmajor(B)
+    dK = ctx.colmajor(Kd)
+    assert G._lib.lib.gpr_trsm_upper_trans(ctx.h, ctypes.c_void_p(dK.data_ptr()), n, n,
+                                           ctypes.c_void_p(dB.data_ptr()), 5, n) == 0
+    assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11

@@ -58,6 +58,7 @@ struct gpr_ctx {
   // gpr_fit_predict: 0 = factor, then solve (default); 1 / 2 = solve inside the factorisation
   // on its own stream / on the main stream (GPR_FUSED_RHS; measured slower at C3: 347 vs 334 ms)
   int fused_rhs = 0;
+  int fuse_y = 0;                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   std::vector<hipEvent_t> sync_events;

@@ -103,12 +103,20 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, co
   if (n <= 0 || ldk < n || nrhs <= 0 || ldy < n || !dX || !dy || !dK || !dalpha)
     return set_err(ctx, GPR_E_ARG, "bad args");
   GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  HIP_TRY(ctx, hipMemcpy2DAsync(dalpha, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
+                                (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
   int hinfo = 0;
+  if (ctx->fuse_y) {
+    // z = U^{-T} y solved inside the factorisation (side stream), then the backward sweep
+    RhsSpec rhs{dalpha, nrhs, n, 0};
+    GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
+    if (info) *info = hinfo;
+    if (hinfo != 0) return hinfo;
+    return potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n, /*forward=*/false);
+  }
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo));
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
-  HIP_TRY(ctx, hipMemcpy2DAsync(dalpha, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
-                                (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
   GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
   return 0;
 }

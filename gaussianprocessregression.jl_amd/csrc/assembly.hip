@@ -560,7 +560,7 @@ void launch_cross(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, cons
 
 // ---- Gram form of the distance on FP64 MFMA ---------------------------------------------
 // -D_ab = (-|y_a|^2 - |y_b|^2) + sum_k (2 y_a,k) y_b,k with y = x .* l - c, where c is the mean of
-// the part's scaled training points (distances are translation invariant; centring keeps |y|^2,
+// (a bounded sample of) the part's scaled training points (distances are translation invariant; centring keeps |y|^2,
 // the cancelling terms, small).  Per 16 x 16 block the sum is ceil(d/4) v_mfma_f64_16x16x4f64
 // started from C = -|y_a|^2 - |y_b|^2 (one VALU add per element), so the FP64 VALU is left with
 // exp (kexp_s2) and the part sum.  Rounding: |error of D| <~ (d + 1) u (|y_a|^2 + |y_b|^2),
@@ -578,20 +578,24 @@ typedef double gd4 __attribute__((ext_vector_type(4)));
 #define GRAM_EXPG 4
 #endif
 
-// grid = nse * d workgroups of 256: c[p][k] = mean_a xs[p][a][k] (fixed-order tree sum)
+// grid = nse * d workgroups of 256: c[p][k] = mean over the first min(n, GRAM_CENTER_PTS) points
+// of xs[p][.][k] (fixed-order tree sum).  Any centre inside the data's spread serves (it only
+// sets the size of |y|^2); a bounded sample keeps this a few microseconds at any n.
+constexpr int GRAM_CENTER_PTS = 2048;
 __global__ __launch_bounds__(256) void gram_center_kernel(const double* __restrict__ xs, int n,
                                                           int d, double* __restrict__ c) {
   __shared__ double red[256];
   const int p = blockIdx.x / d, k = blockIdx.x % d;
+  const int cnt = min(n, GRAM_CENTER_PTS);
   double sum = 0.0;
-  for (int a = threadIdx.x; a < n; a += 256) sum += xs[((size_t)p * n + a) * d + k];
+  for (int a = threadIdx.x; a < cnt; a += 256) sum += xs[((size_t)p * n + a) * d + k];
   red[threadIdx.x] = sum;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) c[p * KMAXD + k] = red[0] / (double)n;
+  if (threadIdx.x == 0) c[p * KMAXD + k] = red[0] / (double)cnt;
 }
 
 // out[p][blk][s][lane] = scale * y[16 blk + (lane & 15)][4 s + (lane >> 4)] (0 past d or n);

@@ -58,7 +58,8 @@ struct gpr_ctx {
   // gpr_fit_predict: 0 = factor, then solve (default); 1 / 2 = solve inside the factorisation
   // on its own stream / on the main stream (GPR_FUSED_RHS; measured slower at C3: 347 vs 334 ms)
   int fused_rhs = 0;
-  int fuse_y = 0;                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
+  int fuse_y = 0;
+  int fuse_kinv = 1;              // gpr_fit_kinv: Z = U^{-T} solved inside the factorisation                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   std::vector<hipEvent_t> sync_events;
@@ -195,6 +196,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
 int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs);
+int kinv_from_z(gpr_ctx* ctx, const double* Z, int n, double* dKinv, int ldk);
 // norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream
 int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm);
 // forward = false: only the backward sweep U x = B (B already holds U^{-T} b)

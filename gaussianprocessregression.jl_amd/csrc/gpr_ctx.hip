@@ -155,6 +155,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   }
   if (const char* e = getenv("GPR_FUSED_RHS")) ctx->fused_rhs = atoi(e);
   if (const char* e = getenv("GPR_FUSE_Y")) ctx->fuse_y = atoi(e);
+  if (const char* e = getenv("GPR_FUSE_KINV")) ctx->fuse_kinv = atoi(e);
   if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
   if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
   if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);

@@ -1880,6 +1880,13 @@ int gpr_potri_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dKi
   double* Z = ctx->dbig;
   GPR_TRY(launch_set_identity(ctx, Z, n, n));
   GPR_TRY(trsm_ut_core(ctx, dU, n, ldu, Z, n, n, nullptr, 1));  // Z = U^{-T}
+  return kinv_from_z(ctx, Z, n, dKinv, ldk);
+}
+
+}  // extern "C"
+
+// K^{-1} = Z^T Z (upper, round-robin K-range SYRK) mirrored to the full matrix, Z = U^{-T}
+int kinv_from_z(gpr_ctx* ctx, const double* Z, int n, double* dKinv, int ldk) {
   GemmArgs g{};
   g.P = Z; g.ldp = n;
   g.Q = Z; g.ldq = n;
@@ -1891,5 +1898,3 @@ int gpr_potri_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dKi
   GPR_TRY(launch_mirror_upper(ctx, dKinv, n, ldk));
   return 0;
 }
-
-}  // extern "C"

@@ -161,6 +161,32 @@ int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d
   return launch_mirror_upper(ctx, dvar, m, ldv);
 }
 
+int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                 const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
+                 double* dK, int ldk, double* dalpha, double* dKinv, int ldkinv, int* info) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (n <= 0 || ldk < n || ldkinv < n || nrhs <= 0 || ldy < n || !dX || !dy || !dK || !dalpha ||
+      !dKinv)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, (size_t)n * n));
+  double* Z = ctx->dbig;
+  GPR_TRY(launch_set_identity(ctx, Z, n, n));
+  HIP_TRY(ctx, hipMemcpy2DAsync(dalpha, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
+                                (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
+  int hinfo = 0;
+  // Z = U^{-T} (identity right-hand side, lower triangular) solved in the factorisation's
+  // lookahead bubbles (GPR_FUSE_KINV=0: after it, as gpr_potri_upper)
+  RhsSpec rhs{Z, n, n, 1};
+  GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, ctx->fuse_kinv ? &rhs : nullptr));
+  if (info) *info = hinfo;
+  if (hinfo != 0) return hinfo;
+  GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
+  if (!ctx->fuse_kinv) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
+  return kinv_from_z(ctx, Z, n, dKinv, ldkinv);
+}
+
 int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                     const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
                     double* dK, int ldk, double* dalpha, const double* dXp, int m, int mode,

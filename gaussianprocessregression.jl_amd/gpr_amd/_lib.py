@@ -62,6 +62,7 @@ _SIGS = {
     "gpr_fit": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _d, _p, _i, _p, _ip]),
     "gpr_predict": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _i, _p, _i, _i, _d, _p, _p,
                          _i, _p]),
+    "gpr_fit_kinv": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _d, _p, _i, _p, _p, _i, _ip]),
     "gpr_fit_predict": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _d, _p, _i, _p, _p, _i, _i,
                              _p, _p, _i, _p, _ip]),
     "gpr_split_predict": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _i, _i,

@@ -349,15 +349,17 @@ def update_cache_(tc: MllLossCache, hp, md: GPRModel, eps: float = EPS_DEFAULT):
     y = md.dsample()
     info = ctypes.c_int(0)
     n = md.n
-    rc = lib.gpr_fit(ctx.h, kinds, nk, hpp, md.d, _ptr(md.dx()), n, _ptr(y), 1, n, eps,
-                     _ptr(tc.kchol_base), n, _ptr(tc.alpha), ctypes.byref(info))
-    ctx.check(rc, "gpr_fit")
+    if isinstance(tc, MllGradCache):  # K, U, alpha and K^{-1} in one call (src/cost.jl:83-111)
+        rc = lib.gpr_fit_kinv(ctx.h, kinds, nk, hpp, md.d, _ptr(md.dx()), n, _ptr(y), 1, n, eps,
+                              _ptr(tc.kchol_base), n, _ptr(tc.alpha), _ptr(tc.Kinv), n,
+                              ctypes.byref(info))
+    else:
+        rc = lib.gpr_fit(ctx.h, kinds, nk, hpp, md.d, _ptr(md.dx()), n, _ptr(y), 1, n, eps,
+                         _ptr(tc.kchol_base), n, _ptr(tc.alpha), ctypes.byref(info))
     tc.info = info.value
     if info.value != 0:
         raise PosDefException(info.value)
-    if isinstance(tc, MllGradCache):
-        ctx.check(lib.gpr_potri_upper(ctx.h, _ptr(tc.kchol_base), n, n, _ptr(tc.Kinv), n),
-                  "gpr_potri_upper")
+    ctx.check(rc, "gpr_fit")
 
 
 def _mll_value(md: GPRModel, tc: MllLossCache) -> float:

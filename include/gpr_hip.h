@@ -153,6 +153,14 @@ int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d
                 int nrhs, const double* dXp, int m, int mode, double eps, double* dmu,
                 double* dvar, int ldv, double* dwork);
 
+/* ---- a5/a6/a7 fused: update_cache!(::MllGradCache) = K, cholesky!, alpha, K^{-1} --------- */
+/* src/cost.jl:83-111 in one call: K into dK (upper -> U, lower keeps K), alpha = K^{-1} y
+ * (n x nrhs), dKinv = full symmetric K^{-1} (ldkinv).  Z = U^{-T} is solved inside the
+ * factorisation (GPR_FUSE_KINV=0: after it), K^{-1} = Z^T Z.  >0: LAPACK info. */
+int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                 const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
+                 double* dK, int ldk, double* dalpha, double* dKinv, int ldkinv, int* info);
+
 /* ---- a5/a6/a10/a11 fused: predict(md, xp; diagonal_var) from scratch ---------------- */
 /* The reference's predict (src/predict.jl:14-25 -> update_cache!(pc, md) :29-34 = K, cholesky!,
  * ldiv!(wt, kchol, md.y), then predict! :36-71) in one call: K(x, x) into dK (upper

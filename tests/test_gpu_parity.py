@@ -612,3 +612,35 @@ def test_fit_predict_multi_output_and_reuse():
     assert G._lib.lib.gpr_trsm_upper_trans(ctx.h, ctypes.c_void_p(dK.data_ptr()), n, n,
                                            ctypes.c_void_p(dB.data_ptr()), 5, n) == 0
     assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("n,nb2", [(300, None), (1300, 256), (2100, 1024), (777, 512)])
+def test_fit_kinv(n, nb2, fuse, monkeypatch):
+    """gpr_fit_kinv = update_cache!(::MllGradCache) (src/cost.jl:83-111): U, alpha and the
+    dense K^{-1}, with Z = U^{-T} solved inside the factorisation (fuse=1) or after it."""
+    monkeypatch.setenv("GPR_FUSE_KINV", fuse)
+    kinds = KSETS["SE+WN"]
+    dim = 4
+    x, y, _ = O.synthetic(dim, n, 0, seed_train=n)
+    hp = O.default_hp(kinds, dim, noise=0.1)
+    ctx = G.Context(0)
+    if nb2:
+        assert G._lib.lib.gpr_set_outer_block(ctx.h, nb2) == 0
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, Kinv, alpha = ctx.empty(n, n), ctx.empty(n, n), ctx.empty(n)
+    karr = (ctypes.c_int * 2)(1, 2)
+    info = ctypes.c_int(-1)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rc = G._lib.lib.gpr_fit_kinv(ctx.h, karr, 2, hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                 dim, P(dx), n, P(dy), 1, n, 1e-8, P(K), n, P(alpha), P(Kinv), n,
+                                 ctypes.byref(info))
+    assert rc == 0 and info.value == 0
+    Ko = O.kernel(kinds, hp, x)
+    Uo = sla.cholesky(Ko, lower=False)
+    Kd = ctx.host(K)
+    assert relnorm(np.triu(Kd), Uo) < 1e-11
+    np.testing.assert_allclose(ctx.host(alpha), O.cho_solve_upper(Uo, y), rtol=1e-9, atol=1e-12)
+    Ki = ctx.host(Kinv)
+    assert np.array_equal(Ki, Ki.T)
+    assert relnorm(Ki, O.kinv_from_upper(Uo)) < 1e-10

@@ -1492,6 +1492,10 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   }
   hipStream_t user = ctx->stream;
   hipStream_t s0 = ctx->smain ? ctx->smain : ctx->stream, s1 = ctx->stream2;
+  // with fused right-hand sides the trailing updates may run on a high-priority stream so the
+  // (normal-priority) solve only takes CUs the factorisation leaves idle (GPR_RHS_LOWPRIO=1)
+  static const bool rhs_lowprio = getenv("GPR_RHS_LOWPRIO") && atoi(getenv("GPR_RHS_LOWPRIO"));
+  if (rhs && rhs_lowprio && ctx->stream3 && !ctx->inner_la) s0 = ctx->stream3;
   HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), user));
   size_t ev = 0;
   ctx->ev_next = 1000;  // events of the diag hops use a separate index range

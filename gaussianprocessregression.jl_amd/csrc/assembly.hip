@@ -931,13 +931,16 @@ int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int 
   if (same) {
     const double el = (double)n * n;
     TimerScope ts(ctx, TC_KBUILD, el * 8.0);  // "flops" slot carries algorithmic bytes
-    if (gram_enabled(kp.d)) return launch_gram_any(ctx, kp, ctx->dxs, n, nullptr, n, 1, dK, ldk);
+    // (the Gram kernels store 16-B pairs: 16-B aligned K with an even ldk, else difference form)
+    if (gram_enabled(kp.d) && vec_store_ok(dK, ldk))
+      return launch_gram_any(ctx, kp, ctx->dxs, n, nullptr, n, 1, dK, ldk);
     DISPATCH_D(launch_sym, ctx, kp, ctx->dxs, n, dK, ldk);
     LAUNCH_CHECK(ctx);
   } else {
     GPR_TRY(scale_inputs(ctx, kp, dXp, m, &ctx->dxps, &ctx->xps_cap));
     TimerScope ts(ctx, TC_OTHER, 0.0);
-    if (gram_enabled(kp.d)) return launch_gram_any(ctx, kp, ctx->dxs, n, ctx->dxps, m, 0, dK, ldk);
+    if (gram_enabled(kp.d) && vec_store_ok(dK, ldk))
+      return launch_gram_any(ctx, kp, ctx->dxs, n, ctx->dxps, m, 0, dK, ldk);
     DISPATCH_D(launch_cross, ctx, kp, ctx->dxs, n, ctx->dxps, m, dK, ldk);
     LAUNCH_CHECK(ctx);
   }

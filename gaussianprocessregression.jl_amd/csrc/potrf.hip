@@ -961,6 +961,30 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// SWEEP_SC1 (default): the hand-off vector is written and read ONLY with sc1 (L2-coherent,
+// write-through) accesses and the counter is an sc1 store polled by sc1 loads, each polling
+// wave loading only after its own poll matched -- MI355X_MICROARCH.md's first sc1 hand-off
+// row (hipMalloc memory, one workgroup per CU), which needs neither the producer's L2
+// write-back (release, 1.7-6.5 us) nor the consumer's L1 invalidate (acquire, 1.7-7 us) on
+// each of the 256 hops of a sweep.  SWEEP_SC1=0: plain accesses behind agent fences.
+#ifndef SWEEP_SC1
+#define SWEEP_SC1 1
+#endif
+__device__ __forceinline__ double hand_ld(const double* p) {
+#if SWEEP_SC1
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void hand_st(double* p, double v) {
+#if SWEEP_SC1
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+
 // Block until at least `need` blocks are published; `known` caches the last observed count.
 __device__ __forceinline__ void sweep_wait(int* sync, int need, int& known, int lane) {
   if (known >= need) return;
@@ -970,16 +994,23 @@ __device__ __forceinline__ void sweep_wait(int* sync, int need, int& known, int 
       __builtin_amdgcn_s_sleep(1);
   }
   known = __shfl(v, 0);
+#if SWEEP_SC1
+  // no instruction: keeps the compiler from hoisting the sc1 hand-off loads above the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 
 __device__ __forceinline__ void sweep_publish(int* sync, int value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
   __syncthreads();
   if (threadIdx.x == 0) {
+#if !SWEEP_SC1
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     __hip_atomic_store(&sync[1], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -1027,8 +1058,8 @@ __global__ __launch_bounds__(SW_THREADS) void trsv_fwd_sweep_kernel(
     double z0[NR], z1[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      z0[r] = hand[(size_t)r * n + k * SW_NB + i0];
-      z1[r] = hand[(size_t)r * n + k * SW_NB + i0 + 1];
+      z0[r] = hand_ld(&hand[(size_t)r * n + k * SW_NB + i0]);
+      z1[r] = hand_ld(&hand[(size_t)r * n + k * SW_NB + i0 + 1]);
     }
 #pragma unroll
     for (int jj = 0; jj < SW_COLS; ++jj)
@@ -1054,7 +1085,7 @@ __global__ __launch_bounds__(SW_THREADS) void trsv_fwd_sweep_kernel(
     for (int r = 0; r < NR; ++r) {
       const double s = wave_sum(fma(w0[jj], rs[i0 * NR + r], w1[jj] * rs[(i0 + 1) * NR + r]));
       if (lane == 0 && m < kb) {
-        hand[(size_t)r * n + c0 + m] = s;
+        hand_st(&hand[(size_t)r * n + c0 + m], s);
         B[(size_t)(c0 + m) + (size_t)r * ldb] = s;
       }
     }
@@ -1110,7 +1141,7 @@ __global__ __launch_bounds__(SW_THREADS) void trsv_bwd_sweep_kernel(
       const int j = w * SW_COLS + jj;
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        const double x = j < kk ? hand[(size_t)r * n + k * SW_NB + j] : 0.0;
+        const double x = j < kk ? hand_ld(&hand[(size_t)r * n + k * SW_NB + j]) : 0.0;
         a0[r] = fma(u0[jj], x, a0[r]);
         a1[r] = fma(u1[jj], x, a1[r]);
       }
@@ -1156,7 +1187,7 @@ __global__ __launch_bounds__(SW_THREADS) void trsv_bwd_sweep_kernel(
     double s = 0.0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) s += part[q][idx];
-    hand[(size_t)r * n + r0 + i] = s;
+    hand_st(&hand[(size_t)r * n + r0 + i], s);
     B[(size_t)(r0 + i) + (size_t)r * ldb] = s;
   }
   (void)ok0;

@@ -263,6 +263,41 @@ def test_potrs_repeated_sweeps_identical():
     assert relnorm(outs[0], Xo) < 1e-11
 
 
+def test_potrs_sweeps_under_uneven_load():
+    """MI355X guide: test every inter-workgroup hand-off under UNEVEN load with L1-warm
+    consumers.  The sweeps (sc1 hand-off vector + counter) run on one context while a second
+    context keeps the GPU busy with a factorisation (uneven CU occupancy, other XCDs' L2s
+    dirty); every result must be bit-identical to an idle-GPU run."""
+    n = 4100
+    ctx = G.Context(0)
+    A = _spd(n, seed=21)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    B = np.random.default_rng(4).random((n, 3))
+    dB = ctx.colmajor(B)
+    assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                      ctypes.c_void_p(dB.data_ptr()), 3, n) == 0
+    ref = ctx.host(dB)
+    Xo = O.cho_solve_upper(sla.cholesky(A, lower=False), B)
+    assert relnorm(ref, Xo) < 1e-11
+    import torch
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        M1 = torch.rand(6144, 6144, dtype=torch.float64, device="cuda")
+    side.synchronize()
+    for it in range(6):
+        # background FP64 GEMMs on another stream, not synchronised with the solves
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                M1 = (M1 @ M1) * (1.0 / 6144)
+        for _ in range(3):
+            dB = ctx.colmajor(B)
+            assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                              ctypes.c_void_p(dB.data_ptr()), 3, n) == 0
+            assert np.array_equal(ctx.host(dB), ref), f"iteration {it}: hand-off result differs"
+    side.synchronize()
+
+
 @pytest.mark.parametrize("n", [100, 300, 513])
 def test_potri_and_trsm(n):
     ctx = G.Context(0)

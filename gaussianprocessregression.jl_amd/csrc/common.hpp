@@ -199,6 +199,7 @@ int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int
 int kinv_from_z(gpr_ctx* ctx, const double* Z, int n, double* dKinv, int ldk);
 // norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream
 int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm);
-// forward = false: only the backward sweep U x = B (B already holds U^{-T} b)
+// forward = false: only the backward sweep U x = B (B already holds U^{-T} b);
+// backward = false: only the forward sweep U^T z = B
 int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs, int ldb,
-               bool forward = true);
+               bool forward = true, bool backward = true);

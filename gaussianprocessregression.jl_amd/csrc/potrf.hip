@@ -1197,12 +1197,13 @@ __global__ __launch_bounds__(SW_THREADS) void trsv_bwd_sweep_kernel(
 
 template <int NR>
 static void launch_sweeps(gpr_ctx* ctx, const double* U, size_t ldu, int n, double* B,
-                          size_t ldb, int* sync, bool forward) {
+                          size_t ldb, int* sync, bool forward, bool backward) {
   const int nblk = (n + SW_NB - 1) / SW_NB;
   if (forward)
     trsv_fwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
                                                                     ctx->dtrsv, sync);
-  trsv_bwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
+  if (backward)
+    trsv_bwd_sweep_kernel<NR><<<nblk, SW_THREADS, 0, ctx->stream>>>(U, ldu, n, ctx->winv, B, ldb,
                                                                   ctx->dtrsv, sync + 2);
 }
 
@@ -1825,7 +1826,7 @@ int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int
 
 // B <- K^{-1} B with small nrhs (dpotrs): blocked forward U^T z = b, backward U x = z.
 int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs, int ldb,
-               bool forward) {
+               bool forward, bool backward) {
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   const int nb = ctx->nb;
   const int nblk = (n + nb - 1) / nb;
@@ -1838,9 +1839,9 @@ int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
       HIP_TRY(ctx, hipMemsetAsync(sync, 0, 4 * sizeof(int), ctx->stream));
       TimerScope ts(ctx, TC_OTHER, 0.0);
       if (nc == 1)
-        launch_sweeps<1>(ctx, dU, ldu, n, B, ldb, sync, forward);
+        launch_sweeps<1>(ctx, dU, ldu, n, B, ldb, sync, forward, backward);
       else
-        launch_sweeps<2>(ctx, dU, ldu, n, B, ldb, sync, forward);
+        launch_sweeps<2>(ctx, dU, ldu, n, B, ldb, sync, forward, backward);
       LAUNCH_CHECK(ctx);
     }
     return 0;
@@ -1863,7 +1864,7 @@ int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
       }
     }
     // backward
-    for (int b = nblk - 1; b >= 0; --b) {
+    for (int b = nblk - 1; backward && b >= 0; --b) {
       const int k = b * nb, kb = std::min(nb, n - k);
       const double* wk = ctx->winv + (size_t)b * nb * nb;
       trsv_diag_kernel<<<1, 256, 0, ctx->stream>>>(wk, nb, kb, B + k, (size_t)ldb, nc, 0);

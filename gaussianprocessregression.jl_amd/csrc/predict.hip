@@ -91,6 +91,39 @@ double diag_prior(const int* kinds, int nk, const double* hp, int d) {
   return s;
 }
 
+// ---- Bayesian quadrature of the posterior (src/integrate.jl) ------------------------------
+constexpr double RT_PI_BY_2 = 0.88622692545275801365;  // sqrt(pi) / 2
+
+// erf(x, y) = erf(y) - erf(x), evaluated through erfc where both arguments lie on the same
+// side beyond 1/sqrt(2) (no cancellation of two values near +-1), as SpecialFunctions' two-
+// argument erf the reference calls (src/integrate.jl:4,26)
+__host__ __device__ inline double erf_diff(double x, double y) {
+  const double t = 0.70710678118654752440;
+  if (x > t && y > t) return erfc(x) - erfc(y);
+  if (x < -t && y < -t) return erfc(-y) - erfc(-x);
+  return erf(y) - erf(x);
+}
+
+// k1[j] = prefac * prod_i erf(l_i (a_i - x_ij), l_i (b_i - x_ij))  (antideriv!, :16-31)
+__global__ void antideriv_se_kernel(const double* __restrict__ X, int n, int d, KParams kp,
+                                    const double* __restrict__ ab, double prefac,
+                                    double* __restrict__ k1) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    double v = 1.0;
+    for (int i = 0; i < d; ++i) {
+      const double l = kp.l[0][i], x = X[(size_t)j * d + i];
+      v *= erf_diff(l * (ab[i] - x), l * (ab[d + i] - x));
+    }
+    k1[j] = v * prefac;
+  }
+}
+
+// erf_integ(w, a, b) (src/integrate.jl:6-7): the double integral of exp(-w^2 (x - y)^2)
+double erf_integ(double w, double a, double b) {
+  return 1.0 / (w * w) * (std::exp(-(w * (b - a)) * (w * (b - a))) - 1.0) +
+         2.0 * (RT_PI_BY_2 / w) * (b - a) * std::erf(w * (b - a));
+}
+
 }  // namespace
 
 extern "C" {
@@ -255,6 +288,71 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   g.upper = 1;
   GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
   return launch_mirror_upper(ctx, dvar, m, ldv);
+}
+
+int gpr_antideriv_se(gpr_ctx_t ctx, int d, const double* hp, const double* dX, int n,
+                     const double* a, const double* b, double* dk1, double* k2) {
+  if (d <= 0 || d > KMAXD || n <= 0 || !hp || !dX || !a || !b)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  // hp[0] = sigma, hp[1..d] = l, whatever kernel they belong to (the reference indexes
+  // md.params the same way, src/integrate.jl:19-22)
+  KParams kp{};
+  kp.d = d;
+  for (int i = 0; i < d; ++i) kp.l[0][i] = hp[1 + i];
+  double prefac = hp[0] * hp[0] * std::pow(RT_PI_BY_2, d);
+  double inv = 1.0;
+  for (int i = 0; i < d; ++i) inv *= 1.0 / hp[1 + i];
+  prefac *= inv;
+  if (k2) {  // antideriv2 (:33-41): integ2 = prod_i erf_integ(l_i, a_i, b_i); * sigma^2
+    double i2 = 1.0;
+    for (int i = 0; i < d; ++i) i2 *= erf_integ(hp[1 + i], a[i], b[i]);
+    *k2 = i2 * hp[0] * hp[0];
+  }
+  if (!dk1) return 0;
+  GPR_TRY(ensure_buf(ctx, &ctx->dscratch, &ctx->scratch_cap, (size_t)2 * d + 2));
+  double hab[2 * KMAXD];
+  for (int i = 0; i < d; ++i) {
+    hab[i] = a[i];
+    hab[d + i] = b[i];
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->dscratch, hab, sizeof(double) * 2 * d, hipMemcpyHostToDevice,
+                              ctx->stream));
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  antideriv_se_kernel<<<blocks, 256, 0, ctx->stream>>>(dX, n, d, kp, ctx->dscratch, prefac, dk1);
+  LAUNCH_CHECK(ctx);
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // hab is a stack array
+  return 0;
+}
+
+int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                  const double* dX, int n, const double* dy, int ny, int ldy, const double* a,
+                  const double* b, double eps, double* dK, int ldk, double* dwt, double* Iout,
+                  double* var) {
+  if (!a || !b || !Iout || !var || !dwt || ny <= 0) return set_err(ctx, GPR_E_ARG, "bad args");
+  // update_cache!(wc, md, hp, nothing) (:64-69): K, cholesky!, wt = K^{-1} y
+  int hinfo = 0;
+  const int rc = gpr_fit(ctx, kinds, nk, hp, d, dX, n, dy, ny, ldy, eps, dK, ldk, dwt, &hinfo);
+  if (rc) return rc;
+  // k1, k2 (update_cache!(ac, ...) :106-110)
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)2 * n + ny + 1));
+  double* k1 = ctx->dbig2;
+  double* tt = k1 + n;
+  double* dI = tt + n;
+  double k2 = 0.0;
+  GPR_TRY(gpr_antideriv_se(ctx, d, hp, dX, n, a, b, k1, &k2));
+  // Iout = wt' k1 (mean_integ_impl! :124-131)
+  colgemv_kernel<<<(ny + 3) / 4, 256, 0, ctx->stream>>>(dwt, (size_t)n, n, ny, k1, (size_t)n, 1,
+                                                        dI, 1);
+  LAUNCH_CHECK(ctx);
+  // var = k2 - ||U^{-T} k1||^2 (var_integ_impl!(.., nothing, ..) :134-147: ldiv!(kchol.L, tt))
+  HIP_TRY(ctx, hipMemcpyAsync(tt, k1, sizeof(double) * n, hipMemcpyDeviceToDevice, ctx->stream));
+  GPR_TRY(potrs_core(ctx, dK, n, ldk, tt, 1, n, /*forward=*/true, /*backward=*/false));
+  GPR_TRY(launch_fill(ctx, dI + ny, 1, k2));
+  GPR_TRY(launch_colnorm_sub(ctx, tt, n, n, 1, dI + ny));
+  HIP_TRY(ctx, hipMemcpyAsync(Iout, dI, sizeof(double) * ny, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(var, dI + ny, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
 }
 
 int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,

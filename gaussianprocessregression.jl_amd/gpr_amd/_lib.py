@@ -67,6 +67,9 @@ _SIGS = {
                              _p, _p, _i, _p, _ip]),
     "gpr_split_predict": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _i, _i,
                                _i, _i, _d, _p, _p]),
+    "gpr_antideriv_se": (_i, [_p, _i, _dp, _p, _i, _dp, _dp, _p, _dp]),
+    "gpr_integrate": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _dp, _dp, _d, _p, _i, _p, _dp,
+                           _dp]),
     "gpr_split_factors": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _i, _i, _p, _p, _p]),
 }
 

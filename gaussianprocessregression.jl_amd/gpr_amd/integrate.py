@@ -1,0 +1,107 @@
+"""Bayesian quadrature of the GP posterior, mirroring
+src/integrate.jl: ``gauss_integ``, ``erf_integ``, ``antideriv``/``antideriv2`` for the
+SquaredExp kernel and ``integrate(md, a, b; sample_noise)``.
+
+The fit, the N-vector of antiderivatives and the triangular solve run on the device
+(``gpr_integrate``: K, POTRF, wt = K^{-1} y, k1 by a HIP kernel, Iout = wt' k1,
+var = k2 - ||U^{-T} k1||^2).  ``gauss_integ``/``erf_integ``/``antideriv2`` are scalar host
+functions, as in the reference.  The ``sample_noise`` path (src/integrate.jl:71-100) needs a
+symmetric eigendecomposition of K on the device and is not built: it raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+
+from . import core as C
+from ._lib import lib
+
+RT_PI_BY_2 = math.sqrt(math.pi) * 0.5
+
+
+def _erf2(x: float, y: float) -> float:
+    """two-argument erf(x, y) = erf(y) - erf(x), via erfc on one side beyond 1/sqrt(2)."""
+    t = math.sqrt(0.5)
+    if x > t and y > t:
+        return math.erfc(x) - math.erfc(y)
+    if x < -t and y < -t:
+        return math.erfc(-y) - math.erfc(-x)
+    return math.erf(y) - math.erf(x)
+
+
+def gauss_integ(*args) -> float:
+    """gauss_integ(a, b) = sqrt(pi)/2 erf(a, b); gauss_integ(xs, w, a, b) = int_a^b
+    exp(-w^2 (x - xs)^2) dx (src/integrate.jl:4-5)."""
+    if len(args) == 2:
+        return RT_PI_BY_2 * _erf2(*args)
+    xs, w, a, b = args
+    return (1.0 / w) * RT_PI_BY_2 * _erf2(w * (a - xs), w * (b - xs))
+
+
+def erf_integ(w: float, a: float, b: float) -> float:
+    """erf_integ(w, a, b) (src/integrate.jl:6-7)."""
+    return 1.0 / w ** 2 * (math.exp(-(w * (b - a)) ** 2) - 1.0) + \
+        2.0 * (RT_PI_BY_2 / w) * (b - a) * math.erf(w * (b - a))
+
+
+def antideriv(kern, xs, hp, a, b, ctx: C.Context | None = None) -> np.ndarray:
+    """antideriv(SquaredExp(), xs, hp, a, b) (src/integrate.jl:10-31) on the device."""
+    if not isinstance(kern, C.SquaredExp):
+        raise TypeError("antideriv is defined for SquaredExp only")
+    ctx = ctx or C.default_context()
+    xs = np.asarray(xs, dtype=np.float64)
+    d, n = xs.shape
+    hpa, hpp = C._hp_arr(hp)
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    dx = ctx.colmajor(xs)
+    k1 = ctx.empty(n)
+    ctx.check(lib.gpr_antideriv_se(ctx.h, d, hpp, C._ptr(dx), n, _dp(a), _dp(b), C._ptr(k1),
+                                   None), "gpr_antideriv_se")
+    return ctx.host(k1)
+
+
+def antideriv2(kern, hp, a, b) -> float:
+    """antideriv2(SquaredExp(), hp, a, b) (src/integrate.jl:33-41)."""
+    if not isinstance(kern, C.SquaredExp):
+        raise TypeError("antideriv2 is defined for SquaredExp only")
+    v = 1.0
+    for i in range(len(a)):
+        v *= erf_integ(hp[1 + i], a[i], b[i])
+    return v * hp[0] ** 2
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def integrate(md: C.GPRModel, *args, sample_noise=None, eps: float = C.EPS_DEFAULT):
+    """integrate(md, [hp,] a, b; sample_noise=nothing) -> (Iout, var_Iout)
+    (src/integrate.jl:48-61): Iout has one entry per column of y; var_Iout is the posterior
+    variance of the integral (one value, as the reference's nothing-noise path writes)."""
+    if len(args) == 2:
+        hp, (a, b) = md.params, args
+    else:
+        hp, a, b = args
+    if sample_noise is not None:
+        raise NotImplementedError("integrate(...; sample_noise) needs a device symmetric "
+                                  "eigendecomposition (src/integrate.jl:71-78); not built")
+    ctx = md.ctx
+    kinds, nk = C._kinds_arr(md.covar)
+    hpa, hpp = C._hp_arr(hp)
+    n = md.n
+    ny = 1 if md.y.ndim == 1 else md.y.shape[1]
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    K = ctx.empty(n, n)
+    wt = ctx.empty(ny, n)
+    Iout = np.zeros(ny)
+    var = np.zeros(1)
+    rc = lib.gpr_integrate(ctx.h, kinds, nk, hpp, md.d, C._ptr(md.dx()), n, C._ptr(md.dy()), ny, n,
+                           _dp(a), _dp(b), eps, C._ptr(K), n, C._ptr(wt), _dp(Iout), _dp(var))
+    if rc > 0:
+        raise C.PosDefException(rc)
+    ctx.check(rc, "gpr_integrate")
+    return Iout, np.full(ny, var[0])

@@ -174,6 +174,22 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
                     double* dK, int ldk, double* dalpha, const double* dXp, int m, int mode,
                     double* dmu, double* dvar, int ldv, double* dwork, int* info);
 
+/* ---- 8(f) rank 3: Bayesian quadrature of the posterior (src/integrate.jl) ------------- */
+/* antideriv!(k1, SquaredExp(), x, hp, a, b) and antideriv2 (src/integrate.jl:16-46): dk1[n]
+ * = sigma^2 (sqrt(pi)/2)^d prod(1/l) prod_i erf(l_i (a_i - x_i), l_i (b_i - x_i)) on the
+ * device, *k2 = sigma^2 prod_i erf_integ(l_i, a_i, b_i) (host); hp[0] = sigma, hp[1..d] = l
+ * (the first d + 1 entries, as the reference indexes md.params).  a, b: host d-vectors;
+ * dk1 or k2 may be NULL. */
+int gpr_antideriv_se(gpr_ctx_t ctx, int d, const double* hp, const double* dX, int n,
+                     const double* a, const double* b, double* dk1, double* k2);
+/* integrate(md, hp, a, b; sample_noise=nothing) (src/integrate.jl:48-167): fit (K into dK ->
+ * U, dwt = K^{-1} y, n x ny), Iout[ny] = wt' k1, *var = k2 - ||U^{-T} k1||^2 (host outputs).
+ * The sample_noise path (symmetric eigendecomposition, :71-78) is not provided. */
+int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                  const double* dX, int n, const double* dy, int ny, int ldy, const double* a,
+                  const double* b, double eps, double* dK, int ldk, double* dwt, double* Iout,
+                  double* var);
+
 /* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
 /* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).
  * dmu: ne x nq column-major (index e + q*ne, src/split_predict.jl:10-19).

@@ -369,3 +369,66 @@ def default_hp(kinds, d, length=None, sigma=1.0, noise=0.1):
         else:
             hp += [noise]
     return np.array(hp, dtype=np.float64)
+
+
+# ---------------------------------------------------------------------------------------
+# Bayesian quadrature of the posterior (src/integrate.jl), sample_noise = nothing
+# ---------------------------------------------------------------------------------------
+RT_PI_BY_2 = np.sqrt(np.pi) * 0.5
+
+
+def erf2(x, y):
+    """SpecialFunctions' two-argument erf(x, y) = erf(y) - erf(x) (src/integrate.jl:4,26),
+    through erfc on the same side beyond 1/sqrt(2) (no cancellation)."""
+    from scipy.special import erf, erfc
+    x, y = np.asarray(x, dtype=np.float64), np.asarray(y, dtype=np.float64)
+    t = np.sqrt(0.5)
+    return np.where((x > t) & (y > t), erfc(x) - erfc(y),
+                    np.where((x < -t) & (y < -t), erfc(-y) - erfc(-x), erf(y) - erf(x)))
+
+
+def gauss_integ(xs, w, a, b):
+    """gauss_integ(xs, w, a, b) src/integrate.jl:4-5: int_a^b exp(-w^2 (x - xs)^2) dx."""
+    return (1.0 / w) * RT_PI_BY_2 * erf2(w * (a - xs), w * (b - xs))
+
+
+def erf_integ(w, a, b):
+    """erf_integ src/integrate.jl:6-7: int_a^b int_a^b exp(-w^2 (x - y)^2) dx dy."""
+    from scipy.special import erf
+    return 1.0 / w ** 2 * (np.exp(-(w * (b - a)) ** 2) - 1.0) + \
+        2.0 * (RT_PI_BY_2 / w) * (b - a) * erf(w * (b - a))
+
+
+def antideriv_se(xs, hp, a, b):
+    """antideriv!(integ, SquaredExp(), xs, hp, a, b) src/integrate.jl:16-31 (hp[0] = sigma,
+    hp[1..d] = l, the first d + 1 entries of md.params)."""
+    d = xs.shape[0]
+    ls = np.asarray(hp[1:d + 1], dtype=np.float64)
+    prefac = hp[0] ** 2 * (RT_PI_BY_2 ** d) * np.prod(1.0 / ls)
+    integ = np.ones(xs.shape[1])
+    for i in range(d):
+        integ = integ * erf2(ls[i] * (a[i] - xs[i]), ls[i] * (b[i] - xs[i]))
+    return integ * prefac
+
+
+def antideriv2_se(hp, a, b):
+    """antideriv2 src/integrate.jl:33-41."""
+    d = len(a)
+    integ2 = 1.0
+    for i in range(d):
+        integ2 *= erf_integ(hp[1 + i], a[i], b[i])
+    return integ2 * hp[0] ** 2
+
+
+def integrate(kinds, hp, x, y, a, b, eps=EPS_DEFAULT):
+    """integrate(md, hp, a, b; sample_noise=nothing) src/integrate.jl:48-167 ->
+    (Iout[ne], var): wt = K^{-1} y, Iout = wt' k1, var = k2 - ||U^{-T} k1||^2."""
+    K = kernel(kinds, hp, x, None, eps)
+    U = chol_upper(K)
+    Y = y if y.ndim == 2 else y[:, None]
+    wt = cho_solve_upper(U, Y)
+    k1 = antideriv_se(x, hp, a, b)
+    k2 = antideriv2_se(hp, a, b)
+    import scipy.linalg as sla
+    tt = sla.solve_triangular(U, k1, trans="T", lower=False)
+    return wt.T @ k1, k2 - float(tt @ tt)

@@ -13,6 +13,7 @@
 //                               POTRF panels -- rdiv!(Kxp, U) of src/predict.jl:84 on Kxp^T,
 // with the diagonal variance ||V[:, j]||^2 accumulated in the TRSM's GEMM epilogue
 // (src/predict.jl:89-95 without a second pass over V).
+#include <algorithm>
 #include <cmath>
 
 #include "common.hpp"
@@ -122,6 +123,47 @@ __global__ void antideriv_se_kernel(const double* __restrict__ X, int n, int d, 
 double erf_integ(double w, double a, double b) {
   return 1.0 / (w * w) * (std::exp(-(w * (b - a)) * (w * (b - a))) - 1.0) +
          2.0 * (RT_PI_BY_2 / w) * (b - a) * std::erf(w * (b - a));
+}
+
+
+// ---- cross-validation (src/crossval.jl, losses src/loss_grad.jl:12-30) ---------------------
+// xo[:, j] = X[:, idx[j]], yo[j] = y[idx[j]] (the views x[:, tst[i]] etc. of cv_batch :27-30);
+// indices were range-checked on the host.
+__global__ void cv_gather_kernel(const double* __restrict__ X, const double* __restrict__ y, int d,
+                                 const int* __restrict__ idx, int m, double* __restrict__ xo,
+                                 double* __restrict__ yo) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < m * (d + 1); t += gridDim.x * blockDim.x) {
+    const int j = t / (d + 1), i = t - j * (d + 1);
+    const size_t src = (size_t)idx[j];
+    if (i < d) xo[(size_t)j * d + i] = X[src * d + i];
+    else yo[j] = y[src];
+  }
+}
+
+// One workgroup: mode GPR_COST_MSE -> sum((yt - yp)^2) / m; GPR_COST_CHISQ -> sum((yt - yp)^2 /
+// S_ii); 0 -> sum(yp^2) (yp = L^{-1} (y - yp), Mahalanobis); -1 -> yp <- yt - yp, no reduction.
+__global__ __launch_bounds__(256) void cv_loss_kernel(const double* __restrict__ yt,
+                                                      double* __restrict__ yp,
+                                                      const double* __restrict__ S, size_t lds,
+                                                      int m, int mode, double* __restrict__ out) {
+  __shared__ double part[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < m; i += 256) {
+    if (mode == -1) {
+      yp[i] = yt[i] - yp[i];
+      continue;
+    }
+    const double r = mode == 0 ? yp[i] : yt[i] - yp[i];
+    s += mode == GPR_COST_CHISQ ? r * r / S[(size_t)i * lds + i] : r * r;
+  }
+  if (mode == -1) return;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double t = (part[0] + part[1]) + (part[2] + part[3]);
+    *out = mode == GPR_COST_MSE ? t / m : t;
+  }
 }
 
 }  // namespace
@@ -351,6 +393,77 @@ int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int
   GPR_TRY(launch_colnorm_sub(ctx, tt, n, n, 1, dI + ny));
   HIP_TRY(ctx, hipMemcpyAsync(Iout, dI, sizeof(double) * ny, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(var, dI + ny, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                 const double* dX, int n, const double* dy, const int* trn, int ntrn,
+                 const int* tst, int ntst, int nfold, int cost, double eps, double* lss) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (n <= 0 || ntrn <= 0 || ntst <= 0 || nfold <= 0 || !dX || !dy || !trn || !tst || !lss)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  if (cost != GPR_COST_MSE && cost != GPR_COST_CHISQ && cost != GPR_COST_MAHALANOBIS)
+    return set_err(ctx, GPR_E_ARG, "unknown cost");
+  const size_t nidx = (size_t)nfold * (ntrn + ntst);
+  for (size_t f = 0; f < (size_t)nfold; ++f) {
+    for (int j = 0; j < ntrn; ++j)
+      if (trn[f * ntrn + j] < 0 || trn[f * ntrn + j] >= n)
+        return set_err(ctx, GPR_E_ARG, "training index out of range");
+    for (int j = 0; j < ntst; ++j)
+      if (tst[f * ntst + j] < 0 || tst[f * ntst + j] >= n)
+        return set_err(ctx, GPR_E_ARG, "test index out of range");
+  }
+  // workspace (ctx->dbig, not touched by the fit/predict calls below): K (ntrn^2), Sigma_p
+  // (ntst^2), xtrn, xtst, ytrn, ytst, yp, lss, then the int indices
+  const size_t szK = (size_t)ntrn * ntrn, szS = (size_t)ntst * ntst;
+  const size_t szv = (size_t)d * (ntrn + ntst) + ntrn + 2 * (size_t)ntst + nfold;
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, szK + szS + szv + (nidx + 1) / 2));
+  double* K = ctx->dbig;
+  double* S = K + szK;
+  double* xtr = S + szS;
+  double* xts = xtr + (size_t)d * ntrn;
+  double* ytr = xts + (size_t)d * ntst;
+  double* yts = ytr + ntrn;
+  double* yp = yts + ntst;
+  double* dl = yp + ntst;
+  int* di = reinterpret_cast<int*>(dl + nfold);
+  std::vector<int> hidx(nidx);
+  std::copy(trn, trn + (size_t)nfold * ntrn, hidx.begin());
+  std::copy(tst, tst + (size_t)nfold * ntst, hidx.begin() + (size_t)nfold * ntrn);
+  HIP_TRY(ctx, hipMemcpyAsync(di, hidx.data(), nidx * sizeof(int), hipMemcpyHostToDevice,
+                              ctx->stream));
+  for (int f = 0; f < nfold; ++f) {
+    const int* itr = di + (size_t)f * ntrn;
+    const int* its = di + (size_t)nfold * ntrn + (size_t)f * ntst;
+    cv_gather_kernel<<<std::min((ntrn * (d + 1) + 255) / 256, 1024), 256, 0, ctx->stream>>>(
+        dX, dy, d, itr, ntrn, xtr, ytr);
+    LAUNCH_CHECK(ctx);
+    cv_gather_kernel<<<std::min((ntst * (d + 1) + 255) / 256, 1024), 256, 0, ctx->stream>>>(
+        dX, dy, d, its, ntst, xts, yts);
+    LAUNCH_CHECK(ctx);
+    // cv_step! (:46-51): update_cache!(pc, mdt) + predict!(yp, Sigma_p, mdt, xtst, pc)
+    int hinfo = 0;
+    const int rc = gpr_fit_predict(ctx, kinds, nk, hp, d, xtr, ntrn, ytr, 1, ntrn, eps, K, ntrn,
+                                   nullptr, xts, ntst, GPR_PREDICT_FULL, yp, S, ntst, nullptr,
+                                   &hinfo);
+    if (rc) return rc;
+    if (cost == GPR_COST_MAHALANOBIS) {
+      // delta = y - yp; cholesky(Sigma_p); ldiv!(L, delta); dot(delta, delta) (:25-30).
+      // Sigma_p = U^T U, so L^{-1} = U^{-T}: the forward sweep
+      cv_loss_kernel<<<1, 256, 0, ctx->stream>>>(yts, yp, S, ntst, ntst, -1, nullptr);
+      LAUNCH_CHECK(ctx);
+      GPR_TRY(potrf_core(ctx, S, ntst, ntst, &hinfo));
+      if (hinfo != 0) return hinfo;
+      GPR_TRY(potrs_core(ctx, S, ntst, ntst, yp, 1, ntst, /*forward=*/true, /*backward=*/false));
+      cv_loss_kernel<<<1, 256, 0, ctx->stream>>>(yts, yp, S, ntst, ntst, 0, dl + f);
+    } else {
+      cv_loss_kernel<<<1, 256, 0, ctx->stream>>>(yts, yp, S, ntst, ntst, cost, dl + f);
+    }
+    LAUNCH_CHECK(ctx);
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(lss, dl, sizeof(double) * nfold, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return 0;
 }

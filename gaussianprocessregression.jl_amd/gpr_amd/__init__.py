@@ -39,6 +39,7 @@ from .core import (
     update_cache_,
 )
 
+from .crossval import ChiSq, Mahalanobis, MSE, cv_batch, cv_step, cv_step_, kfoldcv
 from .integrate import antideriv, antideriv2, erf_integ, gauss_integ, integrate
 from .train import (
     BFGS,

@@ -23,6 +23,9 @@ GPR_WN = 2
 GPR_PREDICT_MEAN = 0
 GPR_PREDICT_DIAG = 1
 GPR_PREDICT_FULL = 2
+GPR_COST_MSE = 1
+GPR_COST_CHISQ = 2
+GPR_COST_MAHALANOBIS = 3
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libgpr_hip.so not found at {LIB_PATH}: build it with "
@@ -70,6 +73,7 @@ _SIGS = {
     "gpr_antideriv_se": (_i, [_p, _i, _dp, _p, _i, _dp, _dp, _p, _dp]),
     "gpr_integrate": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _dp, _dp, _d, _p, _i, _p, _dp,
                            _dp]),
+    "gpr_cv_batch": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _ip, _i, _ip, _i, _i, _i, _d, _dp]),
     "gpr_split_factors": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _i, _i, _p, _p, _p]),
 }
 

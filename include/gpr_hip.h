@@ -54,6 +54,11 @@ extern "C" {
 #define GPR_PREDICT_DIAG 1  /* predict(...; diagonal_var=true)                       */
 #define GPR_PREDICT_FULL 2  /* predict(...; diagonal_var=false)                      */
 
+/* cross-validation losses (src/loss_grad.jl:12-30) */
+#define GPR_COST_MSE 1         /* MSE:  sum((y - yp)^2) / length(y)                   */
+#define GPR_COST_CHISQ 2       /* ChiSq: sum((y - yp)^2 / Sigma_p[i, i])              */
+#define GPR_COST_MAHALANOBIS 3 /* Mahalanobis: ||L^{-1}(y - yp)||^2, Sigma_p = L L^T   */
+
 typedef struct gpr_ctx* gpr_ctx_t;
 
 /* ---- context & memory ------------------------------------------------------------- */
@@ -189,6 +194,17 @@ int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int
                   const double* dX, int n, const double* dy, int ny, int ldy, const double* a,
                   const double* b, double eps, double* dK, int ldk, double* dwt, double* Iout,
                   double* var);
+
+/* cv_batch(md, cost, x, y, (trn, tst)) (src/crossval.jl:13-35): for each fold f, fit the
+ * model on the training points trn[f*ntrn .. +ntrn) of (dX, dy) and predict the test points
+ * tst[f*ntst .. +ntst) with the FULL posterior covariance (cv_step!, :46-51 = update_cache!
+ * + predict!), then lss[f] = loss(cost, ytst, yp, Sigma_p) with cost GPR_COST_*.
+ * trn/tst: host arrays of 0-based point indices (< n), fold-major; lss: host, nfold.
+ * dX: d x n column-major, dy: n.  Returns info > 0 if a training K (or, for Mahalanobis,
+ * Sigma_p) is not positive definite -- the reference's PosDefException. */
+int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                 const double* dX, int n, const double* dy, const int* trn, int ntrn,
+                 const int* tst, int ntst, int nfold, int cost, double eps, double* lss);
 
 /* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
 /* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).

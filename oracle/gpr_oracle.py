@@ -432,3 +432,50 @@ def integrate(kinds, hp, x, y, a, b, eps=EPS_DEFAULT):
     import scipy.linalg as sla
     tt = sla.solve_triangular(U, k1, trans="T", lower=False)
     return wt.T @ k1, k2 - float(tt @ tt)
+
+
+# ---------------------------------------------------------------------------------------
+# Cross-validation (src/crossval.jl) and its losses (src/loss_grad.jl:12-30)
+# ---------------------------------------------------------------------------------------
+def kfoldcv(n: int, k: int, nb: int | None = None, perm=None):
+    """kfoldcv(n, k, nb = div(n, k)) src/crossval.jl:1-11 with 0-based indices: perm plays
+    shuffle(1:n); fold i tests perm[i k : (i+1) k] and trains on perm at every OTHER
+    position, in order."""
+    nb = n // k if nb is None else nb
+    perm = np.arange(n) if perm is None else np.asarray(perm)
+    trn, tst = [], []
+    for i in range(nb):
+        pos = np.arange(i * k, (i + 1) * k)
+        tst.append(perm[pos])
+        keep = np.ones(n, dtype=bool)
+        keep[pos] = False
+        trn.append(perm[keep])
+    return trn, tst
+
+
+def cv_loss(cost: str, y, yp, S) -> float:
+    """loss(::MSE | ::ChiSq | ::Mahalanobis, y, yp, Sigma_p) src/loss_grad.jl:12-30."""
+    r = np.asarray(y) - np.asarray(yp)
+    if cost == "MSE":
+        return float(np.sum(r * r) / r.size)
+    if cost == "ChiSq":
+        return float(np.sum(r * r / np.diag(S)))
+    if cost == "Mahalanobis":  # cholesky(Sigma_p) reads the upper triangle (uplo 'U')
+        U = sla.cholesky(S, lower=False, check_finite=False)
+        z = sla.solve_triangular(U, r, trans="T", lower=False, check_finite=False)
+        return float(z @ z)
+    raise ValueError(cost)
+
+
+def cv_step(kinds, hp, cost, xtr, ytr, xtst, ytst, eps=EPS_DEFAULT) -> float:
+    """cv_step / cv_step! src/crossval.jl:37-51: fit on (xtr, ytr), full-covariance predict
+    at xtst, loss(cost, ytst, yp, Sigma_p)."""
+    yp, S = predict(kinds, hp, xtr, ytr, xtst, diagonal_var=False, eps=eps)
+    return cv_loss(cost, ytst, yp, S)
+
+
+def cv_batch(kinds, hp, cost, x, y, cvset, eps=EPS_DEFAULT) -> np.ndarray:
+    """cv_batch(md, cost, x, y, (trn, tst)) src/crossval.jl:13-35."""
+    trn, tst = cvset
+    return np.array([cv_step(kinds, hp, cost, x[:, a], y[a], x[:, b], y[b], eps)
+                     for a, b in zip(trn, tst)])

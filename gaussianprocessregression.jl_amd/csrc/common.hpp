@@ -77,6 +77,10 @@ struct gpr_ctx {
   double* dexptab = nullptr;    // 2^(j/256), j < 256, correctly rounded (assembly exp)
   double* dscratch = nullptr;   // generic scratch (partials, small vectors)
   size_t scratch_cap = 0;       // doubles
+  // child contexts that run cross-validation folds concurrently (gpr_cv_batch)
+  static constexpr int CV_MAX_SUB = 8;
+  struct gpr_ctx* cv_sub[CV_MAX_SUB] = {};
+  int cv_streams = 4;  // GPR_CV_STREAMS
   double* dbig = nullptr;       // large scratch (Z for potri, Kpx for predict, ...)
   size_t big_cap = 0;           // doubles
   double* dbig2 = nullptr;

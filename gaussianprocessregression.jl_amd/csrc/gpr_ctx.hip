@@ -160,6 +160,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
   if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);
   if (const char* e = getenv("GPR_INNER_LA")) ctx->inner_la = atoi(e);
+  if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
   // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is
   // on the critical path of the lookahead chain.  GEMM streams get the complement mask.
@@ -209,6 +210,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
 
 int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (!ctx) return 0;
+  for (auto* sub : ctx->cv_sub) gpr_ctx_destroy(sub);
   hipStreamSynchronize(ctx->stream);
   drain_timing(ctx);
   for (auto e : ctx->event_pool) hipEventDestroy(e);

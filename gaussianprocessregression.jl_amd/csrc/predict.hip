@@ -15,6 +15,7 @@
 // (src/predict.jl:89-95 without a second pass over V).
 #include <algorithm>
 #include <cmath>
+#include <thread>
 
 #include "common.hpp"
 
@@ -397,6 +398,74 @@ int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int
   return 0;
 }
 
+// Folds f0, f0 + fstep, ... of gpr_cv_batch on context c (indices already range-checked);
+// lss is the caller's host array, written only at this context's folds.
+static int cv_folds(gpr_ctx* c, const int* kinds, int nk, const double* hp, int d,
+                    const double* dX, int n, const double* dy, const int* trn, int ntrn,
+                    const int* tst, int ntst, int nfold, int f0, int fstep, int cost, double eps,
+                    double* lss) {
+  const int nmine = (nfold - f0 + fstep - 1) / fstep;
+  const size_t nidx = (size_t)nmine * (ntrn + ntst);
+  // workspace (c->dbig, not touched by the fit/predict calls below): K (ntrn^2), Sigma_p
+  // (ntst^2), xtrn, xtst, ytrn, ytst, yp, losses, then the int indices
+  const size_t szK = (size_t)ntrn * ntrn, szS = (size_t)ntst * ntst;
+  const size_t szv = (size_t)d * (ntrn + ntst) + ntrn + 2 * (size_t)ntst + nmine;
+  GPR_TRY(ensure_buf(c, &c->dbig, &c->big_cap, szK + szS + szv + (nidx + 1) / 2));
+  double* K = c->dbig;
+  double* S = K + szK;
+  double* xtr = S + szS;
+  double* xts = xtr + (size_t)d * ntrn;
+  double* ytr = xts + (size_t)d * ntst;
+  double* yts = ytr + ntrn;
+  double* yp = yts + ntst;
+  double* dl = yp + ntst;
+  int* di = reinterpret_cast<int*>(dl + nmine);
+  std::vector<int> hidx(nidx);
+  for (int i = 0; i < nmine; ++i) {
+    const size_t f = (size_t)f0 + (size_t)i * fstep;
+    std::copy(trn + f * ntrn, trn + (f + 1) * ntrn, hidx.begin() + (size_t)i * ntrn);
+    std::copy(tst + f * ntst, tst + (f + 1) * ntst,
+              hidx.begin() + (size_t)nmine * ntrn + (size_t)i * ntst);
+  }
+  HIP_TRY(c, hipMemcpyAsync(di, hidx.data(), nidx * sizeof(int), hipMemcpyHostToDevice,
+                            c->stream));
+  for (int i = 0; i < nmine; ++i) {
+    const int* itr = di + (size_t)i * ntrn;
+    const int* its = di + (size_t)nmine * ntrn + (size_t)i * ntst;
+    cv_gather_kernel<<<std::min((ntrn * (d + 1) + 255) / 256, 1024), 256, 0, c->stream>>>(
+        dX, dy, d, itr, ntrn, xtr, ytr);
+    LAUNCH_CHECK(c);
+    cv_gather_kernel<<<std::min((ntst * (d + 1) + 255) / 256, 1024), 256, 0, c->stream>>>(
+        dX, dy, d, its, ntst, xts, yts);
+    LAUNCH_CHECK(c);
+    // cv_step! (:46-51): update_cache!(pc, mdt) + predict!(yp, Sigma_p, mdt, xtst, pc)
+    int hinfo = 0;
+    const int rc = gpr_fit_predict(c, kinds, nk, hp, d, xtr, ntrn, ytr, 1, ntrn, eps, K, ntrn,
+                                   nullptr, xts, ntst, GPR_PREDICT_FULL, yp, S, ntst, nullptr,
+                                   &hinfo);
+    if (rc) return rc;
+    if (cost == GPR_COST_MAHALANOBIS) {
+      // delta = y - yp; cholesky(Sigma_p); ldiv!(L, delta); dot(delta, delta) (:25-30).
+      // Sigma_p = U^T U, so L^{-1} = U^{-T}: the forward sweep
+      cv_loss_kernel<<<1, 256, 0, c->stream>>>(yts, yp, S, ntst, ntst, -1, nullptr);
+      LAUNCH_CHECK(c);
+      GPR_TRY(potrf_core(c, S, ntst, ntst, &hinfo));
+      if (hinfo != 0) return hinfo;
+      GPR_TRY(potrs_core(c, S, ntst, ntst, yp, 1, ntst, /*forward=*/true, /*backward=*/false));
+      cv_loss_kernel<<<1, 256, 0, c->stream>>>(yts, yp, S, ntst, ntst, 0, dl + i);
+    } else {
+      cv_loss_kernel<<<1, 256, 0, c->stream>>>(yts, yp, S, ntst, ntst, cost, dl + i);
+    }
+    LAUNCH_CHECK(c);
+  }
+  std::vector<double> hl(nmine);
+  HIP_TRY(c, hipMemcpyAsync(hl.data(), dl, sizeof(double) * nmine, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < nmine; ++i) lss[(size_t)f0 + (size_t)i * fstep] = hl[i];
+  return 0;
+}
+
 int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                  const double* dX, int n, const double* dy, const int* trn, int ntrn,
                  const int* tst, int ntst, int nfold, int cost, double eps, double* lss) {
@@ -406,7 +475,6 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
     return set_err(ctx, GPR_E_ARG, "bad args");
   if (cost != GPR_COST_MSE && cost != GPR_COST_CHISQ && cost != GPR_COST_MAHALANOBIS)
     return set_err(ctx, GPR_E_ARG, "unknown cost");
-  const size_t nidx = (size_t)nfold * (ntrn + ntst);
   for (size_t f = 0; f < (size_t)nfold; ++f) {
     for (int j = 0; j < ntrn; ++j)
       if (trn[f * ntrn + j] < 0 || trn[f * ntrn + j] >= n)
@@ -415,56 +483,36 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
       if (tst[f * ntst + j] < 0 || tst[f * ntst + j] >= n)
         return set_err(ctx, GPR_E_ARG, "test index out of range");
   }
-  // workspace (ctx->dbig, not touched by the fit/predict calls below): K (ntrn^2), Sigma_p
-  // (ntst^2), xtrn, xtst, ytrn, ytst, yp, lss, then the int indices
-  const size_t szK = (size_t)ntrn * ntrn, szS = (size_t)ntst * ntst;
-  const size_t szv = (size_t)d * (ntrn + ntst) + ntrn + 2 * (size_t)ntst + nfold;
-  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, szK + szS + szv + (nidx + 1) / 2));
-  double* K = ctx->dbig;
-  double* S = K + szK;
-  double* xtr = S + szS;
-  double* xts = xtr + (size_t)d * ntrn;
-  double* ytr = xts + (size_t)d * ntst;
-  double* yts = ytr + ntrn;
-  double* yp = yts + ntst;
-  double* dl = yp + ntst;
-  int* di = reinterpret_cast<int*>(dl + nfold);
-  std::vector<int> hidx(nidx);
-  std::copy(trn, trn + (size_t)nfold * ntrn, hidx.begin());
-  std::copy(tst, tst + (size_t)nfold * ntst, hidx.begin() + (size_t)nfold * ntrn);
-  HIP_TRY(ctx, hipMemcpyAsync(di, hidx.data(), nidx * sizeof(int), hipMemcpyHostToDevice,
-                              ctx->stream));
-  for (int f = 0; f < nfold; ++f) {
-    const int* itr = di + (size_t)f * ntrn;
-    const int* its = di + (size_t)nfold * ntrn + (size_t)f * ntst;
-    cv_gather_kernel<<<std::min((ntrn * (d + 1) + 255) / 256, 1024), 256, 0, ctx->stream>>>(
-        dX, dy, d, itr, ntrn, xtr, ytr);
-    LAUNCH_CHECK(ctx);
-    cv_gather_kernel<<<std::min((ntst * (d + 1) + 255) / 256, 1024), 256, 0, ctx->stream>>>(
-        dX, dy, d, its, ntst, xts, yts);
-    LAUNCH_CHECK(ctx);
-    // cv_step! (:46-51): update_cache!(pc, mdt) + predict!(yp, Sigma_p, mdt, xtst, pc)
-    int hinfo = 0;
-    const int rc = gpr_fit_predict(ctx, kinds, nk, hp, d, xtr, ntrn, ytr, 1, ntrn, eps, K, ntrn,
-                                   nullptr, xts, ntst, GPR_PREDICT_FULL, yp, S, ntst, nullptr,
-                                   &hinfo);
-    if (rc) return rc;
-    if (cost == GPR_COST_MAHALANOBIS) {
-      // delta = y - yp; cholesky(Sigma_p); ldiv!(L, delta); dot(delta, delta) (:25-30).
-      // Sigma_p = U^T U, so L^{-1} = U^{-T}: the forward sweep
-      cv_loss_kernel<<<1, 256, 0, ctx->stream>>>(yts, yp, S, ntst, ntst, -1, nullptr);
-      LAUNCH_CHECK(ctx);
-      GPR_TRY(potrf_core(ctx, S, ntst, ntst, &hinfo));
-      if (hinfo != 0) return hinfo;
-      GPR_TRY(potrs_core(ctx, S, ntst, ntst, yp, 1, ntst, /*forward=*/true, /*backward=*/false));
-      cv_loss_kernel<<<1, 256, 0, ctx->stream>>>(yts, yp, S, ntst, ntst, 0, dl + f);
-    } else {
-      cv_loss_kernel<<<1, 256, 0, ctx->stream>>>(yts, yp, S, ntst, ntst, cost, dl + f);
-    }
-    LAUNCH_CHECK(ctx);
+  // A fold below ~8k training points is a latency-bound chain of small launches (diag
+  // block, panel GEMM, update per 128 columns) that leaves most CUs idle, so independent
+  // folds run concurrently, one child context (own streams, own workspace) per host thread.
+  int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), nfold);
+  if (ntrn > 8192) nsub = 1;
+  if (nsub <= 1)
+    return cv_folds(ctx, kinds, nk, hp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, 0, 1, cost,
+                    eps, lss);
+  for (int t = 0; t < nsub; ++t) {
+    if (ctx->cv_sub[t]) continue;
+    const int rc = gpr_ctx_create(ctx->device, nullptr, &ctx->cv_sub[t]);
+    if (rc) return set_err(ctx, rc, "creating a cross-validation child context failed");
+    ctx->cv_sub[t]->nb = ctx->nb;
+    ctx->cv_sub[t]->nb2 = ctx->nb2;
   }
-  HIP_TRY(ctx, hipMemcpyAsync(lss, dl, sizeof(double) * nfold, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // dX / dy written on the parent stream
+  std::vector<int> rcs(nsub, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nsub; ++t)
+    th.emplace_back([&, t] {
+      hipSetDevice(ctx->device);
+      rcs[t] = cv_folds(ctx->cv_sub[t], kinds, nk, hp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold,
+                        t, nsub, cost, eps, lss);
+    });
+  for (auto& x : th) x.join();
+  // a non-PD fold (info > 0) wins over nothing; report the first failing child
+  for (int t = 0; t < nsub; ++t)
+    if (rcs[t] > 0) return rcs[t];
+  for (int t = 0; t < nsub; ++t)
+    if (rcs[t] < 0) return set_err(ctx, rcs[t], "%s", ctx->cv_sub[t]->err.c_str());
   return 0;
 }
 

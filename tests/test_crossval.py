@@ -104,3 +104,22 @@ def test_cv_batch_rejects_bad_indices():
     md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), O.default_hp(["SE", "WN"], 2), x, y)
     with pytest.raises(G.GprError):
         G.cv_batch(md, G.MSE(), x, y, ([np.arange(40)], [np.arange(45, 55)]))
+
+
+@pytest.mark.gpu
+def test_cv_concurrent_folds_bit_identical(monkeypatch):
+    """Folds spread over child contexts (default GPR_CV_STREAMS=4) give exactly the losses of
+    the one-context sequential run: same kernels, per-fold deterministic reductions."""
+    d, n, k = 3, 600, 40
+    x, y = _data(d, n, 21)
+    hp = O.default_hp(["SE", "WN"], d, length=2.0)
+    cvset = G.kfoldcv(n, k, rng=np.random.default_rng(2))
+    out = {}
+    for streams in ("1", "4", "8"):
+        monkeypatch.setenv("GPR_CV_STREAMS", streams)
+        ctx = G.Context(0)
+        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=ctx)
+        out[streams] = G.cv_batch(md, G.Mahalanobis(), x, y, cvset)
+        ctx.close()
+    np.testing.assert_array_equal(out["1"], out["4"])
+    np.testing.assert_array_equal(out["1"], out["8"])

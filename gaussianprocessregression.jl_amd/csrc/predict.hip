@@ -15,6 +15,7 @@
 // (src/predict.jl:89-95 without a second pass over V).
 #include <algorithm>
 #include <cmath>
+#include <functional>
 #include <thread>
 
 #include "common.hpp"
@@ -164,6 +165,17 @@ __global__ __launch_bounds__(256) void cv_loss_kernel(const double* __restrict__
   if (threadIdx.x == 0) {
     const double t = (part[0] + part[1]) + (part[2] + part[3]);
     *out = mode == GPR_COST_MSE ? t / m : t;
+  }
+}
+
+
+// Kj = upper(K) + s I (the triangle POTRF reads), column-major, ld n
+__global__ void shift_upper_kernel(const double* __restrict__ K, size_t ldk, int n, double s,
+                                   double* __restrict__ Kj) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)n * n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % n), j = (int)(t / n);
+    if (i <= j) Kj[t] = K[(size_t)j * ldk + i] + (i == j ? s : 0.0);
   }
 }
 
@@ -398,6 +410,36 @@ int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int
   return 0;
 }
 
+// child contexts for independent per-fold / per-column work (see gpr_cv_batch)
+static int ensure_children(gpr_ctx* ctx, int nsub) {
+  for (int t = 0; t < nsub; ++t) {
+    if (ctx->cv_sub[t]) continue;
+    const int rc = gpr_ctx_create(ctx->device, nullptr, &ctx->cv_sub[t]);
+    if (rc) return set_err(ctx, rc, "creating a child context failed");
+    ctx->cv_sub[t]->nb = ctx->nb;
+    ctx->cv_sub[t]->nb2 = ctx->nb2;
+  }
+  return 0;
+}
+
+// run body(child t) for t < nsub on host threads; first info > 0, else first error
+static int run_children(gpr_ctx* ctx, int nsub, const std::function<int(gpr_ctx*, int)>& body) {
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // inputs written on the parent stream
+  std::vector<int> rcs(nsub, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nsub; ++t)
+    th.emplace_back([&, t] {
+      hipSetDevice(ctx->device);
+      rcs[t] = body(ctx->cv_sub[t], t);
+    });
+  for (auto& x : th) x.join();
+  for (int t = 0; t < nsub; ++t)
+    if (rcs[t] > 0) return rcs[t];
+  for (int t = 0; t < nsub; ++t)
+    if (rcs[t] < 0) return set_err(ctx, rcs[t], "%s", ctx->cv_sub[t]->err.c_str());
+  return 0;
+}
+
 // Folds f0, f0 + fstep, ... of gpr_cv_batch on context c (indices already range-checked);
 // lss is the caller's host array, written only at this context's folds.
 static int cv_folds(gpr_ctx* c, const int* kinds, int nk, const double* hp, int d,
@@ -491,29 +533,79 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   if (nsub <= 1)
     return cv_folds(ctx, kinds, nk, hp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, 0, 1, cost,
                     eps, lss);
-  for (int t = 0; t < nsub; ++t) {
-    if (ctx->cv_sub[t]) continue;
-    const int rc = gpr_ctx_create(ctx->device, nullptr, &ctx->cv_sub[t]);
-    if (rc) return set_err(ctx, rc, "creating a cross-validation child context failed");
-    ctx->cv_sub[t]->nb = ctx->nb;
-    ctx->cv_sub[t]->nb2 = ctx->nb2;
+  GPR_TRY(ensure_children(ctx, nsub));
+  return run_children(ctx, nsub, [&](gpr_ctx* c, int t) {
+    return cv_folds(c, kinds, nk, hp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, t, nsub, cost,
+                    eps, lss);
+  });
+}
+
+// Columns j0, j0 + jstep, ... of gpr_integrate_noise on context c: (K + noise_j I) = U_j^T U_j,
+// wt_j = (K + noise_j I)^{-1} y_j, Iout_j = wt_j' k1, var_j = k2 - ||U_j^{-T} k1||^2.
+static int integ_noise_cols(gpr_ctx* c, const double* K, int ldk, int n, const double* dy,
+                            int ldy, const double* k1, double k2, const double* noise, int ny,
+                            int j0, int jstep, double* Iout, double* var) {
+  const int nmine = (ny - j0 + jstep - 1) / jstep;
+  GPR_TRY(ensure_buf(c, &c->dbig, &c->big_cap, (size_t)n * n + 2 * (size_t)n + 2 * nmine));
+  double* Kj = c->dbig;
+  double* w = Kj + (size_t)n * n;
+  double* t = w + n;
+  double* out = t + n;  // [Iout_i, var_i] per owned column
+  const int blocks = (int)std::min<size_t>(((size_t)n * n + 255) / 256, 4096);
+  for (int i = 0; i < nmine; ++i) {
+    const int j = j0 + i * jstep;
+    shift_upper_kernel<<<blocks, 256, 0, c->stream>>>(K, (size_t)ldk, n, noise[j], Kj);
+    LAUNCH_CHECK(c);
+    int hinfo = 0;
+    GPR_TRY(potrf_core(c, Kj, n, n, &hinfo));
+    if (hinfo != 0) return hinfo;
+    HIP_TRY(c, hipMemcpyAsync(w, dy + (size_t)j * ldy, sizeof(double) * n,
+                              hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(t, k1, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+    GPR_TRY(potrs_core(c, Kj, n, n, w, 1, n));
+    colgemv_kernel<<<1, 256, 0, c->stream>>>(w, (size_t)n, n, 1, k1, (size_t)n, 1, out + 2 * i, 1);
+    LAUNCH_CHECK(c);
+    GPR_TRY(potrs_core(c, Kj, n, n, t, 1, n, /*forward=*/true, /*backward=*/false));
+    GPR_TRY(launch_fill(c, out + 2 * i + 1, 1, k2));
+    GPR_TRY(launch_colnorm_sub(c, t, n, n, 1, out + 2 * i + 1));
   }
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // dX / dy written on the parent stream
-  std::vector<int> rcs(nsub, 0);
-  std::vector<std::thread> th;
-  for (int t = 0; t < nsub; ++t)
-    th.emplace_back([&, t] {
-      hipSetDevice(ctx->device);
-      rcs[t] = cv_folds(ctx->cv_sub[t], kinds, nk, hp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold,
-                        t, nsub, cost, eps, lss);
-    });
-  for (auto& x : th) x.join();
-  // a non-PD fold (info > 0) wins over nothing; report the first failing child
-  for (int t = 0; t < nsub; ++t)
-    if (rcs[t] > 0) return rcs[t];
-  for (int t = 0; t < nsub; ++t)
-    if (rcs[t] < 0) return set_err(ctx, rcs[t], "%s", ctx->cv_sub[t]->err.c_str());
+  std::vector<double> h(2 * (size_t)nmine);
+  HIP_TRY(c, hipMemcpyAsync(h.data(), out, sizeof(double) * 2 * nmine, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < nmine; ++i) {
+    Iout[j0 + i * jstep] = h[2 * i];
+    var[j0 + i * jstep] = h[2 * i + 1];
+  }
   return 0;
+}
+
+int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                        const double* dX, int n, const double* dy, int ny, int ldy,
+                        const double* a, const double* b, const double* noise, double eps,
+                        double* Iout, double* var) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (n <= 0 || ny <= 0 || ldy < n || !dX || !dy || !a || !b || !noise || !Iout || !var)
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  // kernel!(wc.kxx, ...) once (src/integrate.jl:72), k1 / k2 once (:106-110)
+  // (in dbig2: the per-column worker factors K + noise_j I in its context's dbig)
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)n * n + n));
+  double* K = ctx->dbig2;
+  double* k1 = K + (size_t)n * n;
+  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, K, n));
+  double k2 = 0.0;
+  GPR_TRY(gpr_antideriv_se(ctx, d, hp, dX, n, a, b, k1, &k2));
+  int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);
+  if (n > 8192) nsub = 1;
+  if (nsub <= 1) {
+    const int rc = integ_noise_cols(ctx, K, n, n, dy, ldy, k1, k2, noise, ny, 0, 1, Iout, var);
+    return rc;
+  }
+  GPR_TRY(ensure_children(ctx, nsub));
+  return run_children(ctx, nsub, [&](gpr_ctx* c, int t) {
+    return integ_noise_cols(c, K, n, n, dy, ldy, k1, k2, noise, ny, t, nsub, Iout, var);
+  });
 }
 
 int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,

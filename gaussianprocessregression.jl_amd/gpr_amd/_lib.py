@@ -73,6 +73,8 @@ _SIGS = {
     "gpr_antideriv_se": (_i, [_p, _i, _dp, _p, _i, _dp, _dp, _p, _dp]),
     "gpr_integrate": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _dp, _dp, _d, _p, _i, _p, _dp,
                            _dp]),
+    "gpr_integrate_noise": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _dp, _dp, _dp, _d, _dp,
+                                 _dp]),
     "gpr_cv_batch": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _ip, _i, _ip, _i, _i, _i, _d, _dp]),
     "gpr_split_factors": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _i, _i, _p, _p, _p]),
 }

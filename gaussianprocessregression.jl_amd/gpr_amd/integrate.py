@@ -5,8 +5,9 @@ SquaredExp kernel and ``integrate(md, a, b; sample_noise)``.
 The fit, the N-vector of antiderivatives and the triangular solve run on the device
 (``gpr_integrate``: K, POTRF, wt = K^{-1} y, k1 by a HIP kernel, Iout = wt' k1,
 var = k2 - ||U^{-T} k1||^2).  ``gauss_integ``/``erf_integ``/``antideriv2`` are scalar host
-functions, as in the reference.  The ``sample_noise`` path (src/integrate.jl:71-100) needs a
-symmetric eigendecomposition of K on the device and is not built: it raises.
+functions, as in the reference.  ``sample_noise`` (one value per column of y,
+src/integrate.jl:71-100) integrates column j with K + noise_j I: the reference diagonalises K
+once (syevr), the device factors each shifted K with the MFMA POTRF (``gpr_integrate_noise``).
 """
 from __future__ import annotations
 
@@ -86,8 +87,7 @@ def integrate(md: C.GPRModel, *args, sample_noise=None, eps: float = C.EPS_DEFAU
     else:
         hp, a, b = args
     if sample_noise is not None:
-        raise NotImplementedError("integrate(...; sample_noise) needs a device symmetric "
-                                  "eigendecomposition (src/integrate.jl:71-78); not built")
+        return _integrate_noise(md, hp, a, b, sample_noise, eps)
     ctx = md.ctx
     kinds, nk = C._kinds_arr(md.covar)
     hpa, hpp = C._hp_arr(hp)
@@ -105,3 +105,33 @@ def integrate(md: C.GPRModel, *args, sample_noise=None, eps: float = C.EPS_DEFAU
         raise C.PosDefException(rc)
     ctx.check(rc, "gpr_integrate")
     return Iout, np.full(ny, var[0])
+
+
+def _integrate_noise(md: C.GPRModel, hp, a, b, sample_noise, eps: float):
+    """integrate(...; sample_noise::Vector) (src/integrate.jl:71-100,149-162): column j of y
+    is integrated with K + sample_noise[j] I.  A scalar sample_noise has no variance method
+    in the reference (var_integ_impl! reaches inverse_diagonal_update2!(var, lam, P,
+    ::Float64, k1, tmp), which is not defined: MethodError) -- mirrored as TypeError."""
+    noise = np.asarray(sample_noise, dtype=np.float64)
+    if noise.ndim == 0:
+        raise TypeError("integrate(...; sample_noise::Float64): no method "
+                        "inverse_diagonal_update2!(var, lam, P, ::Float64, k1, tmp) "
+                        "(src/integrate.jl:157-162); pass one noise value per column of y")
+    ctx = md.ctx
+    ny = 1 if md.y.ndim == 1 else md.y.shape[1]
+    if noise.shape != (ny,):
+        raise ValueError(f"sample_noise must hold one value per column of y ({ny})")
+    kinds, nk = C._kinds_arr(md.covar)
+    hpa, hpp = C._hp_arr(hp)
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    noise = np.ascontiguousarray(noise)
+    Iout = np.zeros(ny)
+    var = np.zeros(ny)
+    rc = lib.gpr_integrate_noise(ctx.h, kinds, nk, hpp, md.d, C._ptr(md.dx()), md.n,
+                                 C._ptr(md.dy()), ny, md.n, _dp(a), _dp(b), _dp(noise), eps,
+                                 _dp(Iout), _dp(var))
+    if rc > 0:
+        raise C.PosDefException(rc)
+    ctx.check(rc, "gpr_integrate_noise")
+    return Iout, var

@@ -206,6 +206,17 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
                  const double* dX, int n, const double* dy, const int* trn, int ntrn,
                  const int* tst, int ntst, int nfold, int cost, double eps, double* lss);
 
+/* integrate(md, hp, a, b; sample_noise = noise::Vector) (src/integrate.jl:71-100,149-162):
+ * per column j of y (ny columns, noise[j] host), Iout[j] = k1' (K + noise_j I)^{-1} y_j and
+ * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  The reference diagonalises K once (LAPACK
+ * syevr) and applies (Lambda + noise_j)^{-1}; here each shifted matrix is factored by the
+ * MFMA POTRF (same quantities; independent columns run on concurrent child contexts).
+ * Returns info > 0 if some K + noise_j I is not positive definite. */
+int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                        const double* dX, int n, const double* dy, int ny, int ldy,
+                        const double* a, const double* b, const double* noise, double eps,
+                        double* Iout, double* var);
+
 /* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
 /* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).
  * dmu: ne x nq column-major (index e + q*ne, src/split_predict.jl:10-19).

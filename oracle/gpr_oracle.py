@@ -479,3 +479,37 @@ def cv_batch(kinds, hp, cost, x, y, cvset, eps=EPS_DEFAULT) -> np.ndarray:
     trn, tst = cvset
     return np.array([cv_step(kinds, hp, cost, x[:, a], y[a], x[:, b], y[b], eps)
                      for a, b in zip(trn, tst)])
+
+
+def inverse_diagonal_update(lam, P, eps, y):
+    """inverse_diagonal_update!(ABy, lam, P, eps, y, tmp) src/integrate.jl:81-95:
+    P (lam + eps)^{-1} P' y; a vector eps applies eps[j] to column j of y."""
+    eps = np.asarray(eps, dtype=np.float64)
+    Pty = P.T @ y
+    if eps.ndim == 0:
+        return P @ (Pty / (lam + eps) if y.ndim == 1 else Pty / (lam[:, None] + eps))
+    return P @ (Pty / (lam[:, None] + eps[None, :]))
+
+
+def inverse_diagonal_update2(lam, P, eps, y):
+    """inverse_diagonal_update2!(...) src/integrate.jl:97-111: y' (P (lam + eps)^{-1} P') y,
+    one value per entry of a vector eps."""
+    t = (P.T @ y) ** 2
+    eps = np.asarray(eps, dtype=np.float64)
+    if eps.ndim == 0:
+        return float(t @ (1.0 / (lam + eps)))
+    return (1.0 / (lam[None, :] + eps[:, None])) @ t
+
+
+def integrate_noise(kinds, hp, x, y, a, b, noise, eps=EPS_DEFAULT):
+    """integrate(md, hp, a, b; sample_noise = noise::Vector) src/integrate.jl:71-79,149-162:
+    K = P Lambda P' (syevr; here numpy's eigh), wt = P (Lambda + noise_j)^{-1} P' y_j,
+    Iout = wt' k1, var_j = k2 - k1' P (Lambda + noise_j)^{-1} P' k1."""
+    K = kernel(kinds, hp, x, None, eps)
+    lam, P = np.linalg.eigh(K)
+    y2 = y[:, None] if y.ndim == 1 else y
+    noise = np.asarray(noise, dtype=np.float64)
+    wt = inverse_diagonal_update(lam, P, noise, y2)
+    k1 = antideriv_se(x, hp, a, b)
+    k2 = antideriv2_se(hp, a, b)
+    return wt.T @ k1, k2 - inverse_diagonal_update2(lam, P, noise, k1)

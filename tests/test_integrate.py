@@ -5,9 +5,12 @@ quadrature (test/test_integrate.jl:3-35; the reference uses QuadGK, here SciPy's
 quad), and the host mirror's scalar functions.  GPU part: the device antiderivative and
 integrate(md, a, b) against the oracle (rtol 1e-12 / 1e-8), and the integral of the posterior
 mean against a tensor Gauss-Legendre rule over the device's predict_mean (rtol 1e-7).
+sample_noise: the oracle's eigen path (test/test_integrate.jl:47-111 restated on it) against
+the device's shifted factorisations, and the reference's own sample-noise tests (:113-152).
 """
 import numpy as np
 import pytest
+import scipy.linalg as sla
 from scipy import integrate as sint
 
 from oracle import gpr_oracle as O
@@ -71,7 +74,7 @@ def test_integrate_vs_oracle(name, dim, n):
     Io, vo = O.integrate(kinds, hp, x, Y, a, b)
     np.testing.assert_allclose(I, Io, rtol=1e-8, atol=1e-12)
     assert v[0] == pytest.approx(vo, rel=1e-8, abs=1e-10 * O.antideriv2_se(hp, a, b))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(TypeError):  # the reference has no scalar-noise variance method
         G.integrate(md, a, b, sample_noise=1e-5)
 
 
@@ -92,3 +95,85 @@ def test_integral_of_posterior_mean_vs_gauss_legendre():
     W = np.outer(w, w).ravel() * 0.25 * (b[0] - a[0]) * (b[1] - a[1])
     mu = G.predict_mean(md, np.stack([X0.ravel(), X1.ravel()]))
     assert float(W @ mu) == pytest.approx(I[0], rel=1e-7)
+
+
+@pytest.mark.parametrize("n", [100, 200])
+def test_inverse_diagonal_update_oracle(n):
+    """test/test_integrate.jl:47-111 on the oracle's eigen path (scalar and vector noise).
+    The reference shifts L L' by 1e-7; at cond ~1e11 the "exact" solve it compares against is
+    itself good to ~1e-5 only, so the shift here is 1e-4."""
+    rng = np.random.default_rng(n)
+    L = np.tril(rng.random((n, n)))
+    A = L @ L.T + 1e-4 * np.eye(n)
+    lam, P = np.linalg.eigh(A)
+    y = rng.random(n)
+    e = 1e-5
+    ex = np.linalg.solve(A + e * np.eye(n), y)
+    np.testing.assert_allclose(O.inverse_diagonal_update(lam, P, e, y), ex, rtol=1e-6)
+    assert O.inverse_diagonal_update2(lam, P, e, y) == pytest.approx(y @ ex, rel=1e-6)
+    ne = 40
+    ev = 1e-5 * rng.random(ne)
+    Y = rng.random((n, ne))
+    exv = np.stack([np.linalg.solve(A + ev[i] * np.eye(n), Y[:, i]) for i in range(ne)], axis=1)
+    np.testing.assert_allclose(O.inverse_diagonal_update(lam, P, ev, Y), exv, rtol=1e-5)
+    q = np.array([y @ np.linalg.solve(A + ev[i] * np.eye(n), y) for i in range(ne)])
+    np.testing.assert_allclose(O.inverse_diagonal_update2(lam, P, ev, y), q, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,dim,n,ne", [("SE", 2, 150, 7), ("SE+WN", 3, 300, 12),
+                                           ("SE", 4, 1100, 5)])
+def test_integrate_sample_noise_vs_oracle(name, dim, n, ne):
+    kinds = [O.SE] if name == "SE" else [O.SE, O.WN]
+    cov = G.SquaredExp() if name == "SE" else G.SquaredExp() + G.WhiteNoise()
+    rng = np.random.default_rng(dim + n)
+    x = rng.random((dim, n))
+    Y = rng.random((n, ne))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    md = G.GPRModel(cov, hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    noise = 1e-3 * (1.0 + rng.random(ne))
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I, Io, rtol=1e-8)
+    np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,n,k", [(1, 100, 100), (2, 200, 300), (4, 300, 200)])
+def test_integrate_zero_noise_reference(dim, n, k):
+    """test/test_integrate.jl:113-126 (random hp as GPRModel(SquaredExp(), x, y))."""
+    rng = np.random.default_rng(100 * dim + k)
+    x = rng.random((dim, n))
+    y = rng.random((n, k))
+    md = G.GPRModel(G.SquaredExp(), None, x, y, rng=rng)
+    a, b = np.zeros(dim), np.ones(dim)
+    mu, s = G.integrate(md, a, b, sample_noise=None)
+    mu0, s0 = G.integrate(md, a, b, sample_noise=np.zeros(k))
+    np.testing.assert_allclose(mu, mu0, rtol=1e-5)
+    assert s[0] == pytest.approx(s0[1], rel=1e-4)
+    np.testing.assert_allclose(s0[1:], 0.0, atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,n,ne", [(1, 100, 100), (3, 200, 300), (4, 300, 100)])
+def test_integrate_inverse_perturbation_reference(dim, n, ne):
+    """test/test_integrate.jl:128-152: column i against cholesky(K + noise_i I)."""
+    rng = np.random.default_rng(7 * dim + ne)
+    x = rng.random((dim, n))
+    y = rng.random((n, ne))
+    md = G.GPRModel(G.SquaredExp(), None, x, y, rng=rng)
+    noise = 1e-5 * rng.random(ne)
+    a, b = np.zeros(dim), np.ones(dim)
+    mu, S = G.integrate(md, a, b, sample_noise=noise)
+    K = O.kernel([O.SE], md.params, x)
+    k1 = O.antideriv_se(x, md.params, a, b)
+    k2 = O.antideriv2_se(md.params, a, b)
+    mu_ex, S_ex = np.zeros(ne), np.zeros(ne)
+    for i in range(ne):
+        U = O.chol_upper(K + noise[i] * np.eye(n))
+        mu_ex[i] = O.cho_solve_upper(U, y[:, i]) @ k1
+        t = sla.solve_triangular(U, k1, trans="T", lower=False)
+        S_ex[i] = k2 - t @ t
+    np.testing.assert_allclose(mu, mu_ex, rtol=1e-5)
+    np.testing.assert_allclose(S, S_ex, rtol=1e-5)

@@ -77,19 +77,34 @@ __device__ __forceinline__ bool tile_coords(const GemmK& a, int& m0, int& n0) {
   const int L = a.xcd_remap ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3)
                             : bid;
   const int Gm = a.gm, Gn = a.gn;
-  const int sidx = L / (Gm * Gn), wl = L % (Gm * Gn);
-  int SI, SJ;
+  int tm, tn;
   if (g.upper) {  // upper super-tiles SI <= SJ, triangular order
+    const int sidx = L / (Gm * Gn), wl = L % (Gm * Gn);
     int sj = (int)((sqrt(8.0 * sidx + 1.0) - 1.0) * 0.5);
     while ((sj + 1) * (sj + 2) / 2 <= sidx) ++sj;
     while (sj * (sj + 1) / 2 > sidx) --sj;
-    SJ = sj;
-    SI = sidx - sj * (sj + 1) / 2;
+    tm = (sidx - sj * (sj + 1) / 2) * Gm + (wl % Gm);
+    tn = sj * Gn + (wl / Gm);
   } else {
-    SI = sidx % a.super_m;
-    SJ = sidx / a.super_m;
+    // the grid holds exactly tiles_m x tiles_n blocks: column bands of Gn tiles (the last one
+    // narrower), each walked in Gm-row super-tiles (the last one shorter).  A grid padded to
+    // whole super-tiles would put all the empty blocks at the end of the logical order, i.e.
+    // on the last XCD, and overload the other seven (+14 % at 8193 right-hand sides).
+    const int tmn = a.tiles_m, tnn = a.tiles_n;
+    const int SJ = L / (tmn * Gn);
+    const int bw = min(Gn, tnn - SJ * Gn);
+    const int t = L - SJ * tmn * Gn;
+    const int fr = (tmn / Gm) * Gm;  // rows covered by whole super-tiles
+    if (t < fr * bw) {
+      const int SI = t / (Gm * bw), r = t - SI * Gm * bw;
+      tm = SI * Gm + r % Gm;
+      tn = SJ * Gn + r / Gm;
+    } else {
+      const int t2 = t - fr * bw, h = tmn - fr;
+      tm = fr + t2 % h;
+      tn = SJ * Gn + t2 / h;
+    }
   }
-  const int tm = SI * Gm + (wl % Gm), tn = SJ * Gn + (wl / Gm);
   if (tm >= a.tiles_m || tn >= a.tiles_n || (g.upper && tm > tn)) return false;
   m0 = tm * TM;
   n0 = tn * TN;
@@ -519,8 +534,7 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
     flops = (double)g.M * (g.M + 1) * g.K;  // 2 * M(M+1)/2 * K
     if (g.kfrom_n) flops = (double)g.M * g.M * g.M / 3.0;
   } else {
-    nblk = (long long)a.super_m * super_n * a.gm * a.gn;
-    if (g.kend_from_m && !g.mask_upper) nblk = (long long)a.tiles_m * a.tiles_n;  // see tile_coords
+    nblk = (long long)a.tiles_m * a.tiles_n;  // exactly the tiles (see tile_coords)
     flops = 2.0 * g.M * (double)g.N * g.K;
     if (g.kend_from_m)  // upper-triangular P: row m of the product uses K-range [0, m]
       flops = (double)g.N * g.M * (g.M + 1);

@@ -35,8 +35,17 @@ from .core import (
     predict,
     predict_,
     predict_mean,
+    predict_mean_,
     split_factors,
     update_cache_,
+    update_predict_cache_,
+    grad_cache,
+    kernels,
+    loss_cache,
+    loss_grad_cache,
+    predict_cache,
+    rm_noise,
+    similar,
 )
 
 from .crossval import ChiSq, Mahalanobis, MSE, cv_batch, cv_step, cv_step_, kfoldcv

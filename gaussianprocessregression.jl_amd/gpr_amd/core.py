@@ -616,3 +616,73 @@ def split_factors(cov: AbstractKernel, hp, x, cm: Cmap, part: int = 0,
     ctx.check(lib.gpr_split_factors(ctx.h, kinds, nk, hpp, d, _ptr(dx), ns, _ptr(dxe), ne, _ptr(dxq),
                                     nq, part, _ptr(A), _ptr(B), _ptr(C)), "gpr_split_factors")
     return ctx.host(A), ctx.host(B), ctx.host(C)
+
+
+# =========================================================================================
+# Cache constructors and small API pieces the reference exports around the path
+# =========================================================================================
+def loss_cache(cost):
+    """loss_cache(::MarginalLikelihood) = MllLossCache (src/cost.jl:10)."""
+    if not isinstance(cost, MarginalLikelihood):
+        raise TypeError(f"no loss cache for {cost!r}")
+    return MllLossCache
+
+
+def grad_cache(cost):
+    """grad_cache / loss_grad_cache(::MarginalLikelihood) = MllGradCache (src/cost.jl:11-12)."""
+    if not isinstance(cost, MarginalLikelihood):
+        raise TypeError(f"no gradient cache for {cost!r}")
+    return MllGradCache
+
+
+loss_grad_cache = grad_cache
+
+
+def predict_cache(md: GPRModel, xp):
+    """predict_cache(md, xp) (src/predict.jl:1, src/split_predict.jl:1): the cache type."""
+    return GPRSplitPredictCache if isinstance(xp, Cmap) else GPRPredictCache
+
+
+def update_predict_cache_(pc: GPRPredictCache, md: GPRModel, eps: float = EPS_DEFAULT):
+    """update_cache!(pc::GPRPredictCache, md) (src/predict.jl:29-34): K, cholesky!, wt."""
+    _update_predict_cache(pc, md, eps)
+
+
+def predict_mean_(mu: torch.Tensor, md: GPRModel, xp, pc: GPRPredictCache,
+                  eps: float = EPS_DEFAULT):
+    """predict_mean!(mu, md, xp, pc) (src/predict.jl:36-40) from an updated cache."""
+    predict_(mu, None, md, xp, pc, True, mean_only=True, eps=eps)
+
+
+def similar(md: GPRModel, hp, x, y) -> GPRModel:
+    """similar(md, hp, x, y) (src/models.jl:47-49): same kernel, new data."""
+    return GPRModel(md.covar, hp, x, y, train_axis=md.train_axis, ctx=md.ctx)
+
+
+def _part_hps(cov: AbstractKernel, hp, dim: int):
+    hp = np.asarray(hp, dtype=np.float64)
+    out, off = [], 0
+    for k in cov.parts():
+        w = dim + 1 if k.KIND == GPR_SE else 1
+        out.append(hp[off:off + w])
+        off += w
+    return out
+
+
+def kernels(cov: AbstractKernel, hp, x, eps: float = EPS_DEFAULT, ctx: Optional[Context] = None):
+    """kernels(K, hp, x) (src/compose_covar.jl:80-107): one N x N matrix per part of a
+    composed kernel, a 1 x 1 zero for WhiteNoise (alloc_kernels :90-95); [kernel(K, hp, x)]
+    for a single kernel.  Each part's matrix is built on the device."""
+    x = np.asarray(x, dtype=np.float64)
+    x = x[None, :] if x.ndim == 1 else x
+    if not isinstance(cov, ComposedKernel):
+        return [kernel(cov, hp, x, eps=eps, ctx=ctx)]
+    return [np.zeros((1, 1)) if k.KIND == GPR_WN else kernel(k, h, x, eps=eps, ctx=ctx)
+            for k, h in zip(cov.parts(), _part_hps(cov, hp, x.shape[0]))]
+
+
+def rm_noise(cov: AbstractKernel, hps):
+    """rm_noise(K::ComposedKernel, hps) (src/compose_covar.jl:30-33): the parts and per-part
+    hyperparameter vectors without the WhiteNoise entries."""
+    keep = [i for i, k in enumerate(cov.parts()) if k.KIND != GPR_WN]
+    return [cov.parts()[i] for i in keep], [hps[i] for i in keep]

@@ -110,6 +110,36 @@ def test_compose_identities():
         rtol=1e-14)
 
 
+def test_kernels_per_part_and_caches():
+    """kernels(K, hp, x) (src/compose_covar.jl:80-107): one matrix per part, 1x1 zero for
+    WhiteNoise; cache constructors and predict_mean! from an updated GPRPredictCache."""
+    rng = np.random.default_rng(12)
+    dim, n, m = 3, 150, 40
+    x, xp = rng.random((dim, n)), rng.random((dim, m))
+    SEk, WNk = G.SquaredExp(), G.WhiteNoise()
+    hps = rng.uniform(0.5, 2.0, 2 * dim + 3)
+    Ks = G.kernels(SEk + WNk + SEk, hps, x)
+    assert len(Ks) == 3 and Ks[1].shape == (1, 1) and Ks[1][0, 0] == 0.0
+    np.testing.assert_allclose(Ks[0], O.kernel([SE], hps[:dim + 1], x), rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(Ks[2], O.kernel([SE], hps[dim + 2:], x), rtol=1e-13, atol=1e-15)
+    assert len(G.kernels(SEk, hps[:dim + 1], x)) == 1
+    parts, ph = G.rm_noise(SEk + WNk + SEk, ["a", "b", "c"])
+    assert len(parts) == 2 and ph == ["a", "c"]
+    assert G.loss_cache(G.MarginalLikelihood()) is G.MllLossCache
+    assert G.loss_grad_cache(G.MarginalLikelihood()) is G.MllGradCache
+    y = np.sin(x.sum(0)) ** 2
+    md = G.GPRModel(SEk + WNk, hps[:dim + 2], x, y)
+    assert G.predict_cache(md, xp) is G.GPRPredictCache
+    pc = G.predict_cache(md, xp)(md, m)
+    G.update_predict_cache_(pc, md)
+    mu = md.ctx.empty(m)
+    G.predict_mean_(mu, md, xp, pc)
+    mu_o, _ = O.predict([SE, WN], hps[:dim + 2], x, y, xp, diagonal_var=True)
+    np.testing.assert_allclose(md.ctx.host(mu), mu_o, rtol=1e-8, atol=1e-12)
+    md2 = G.similar(md, hps[:dim + 2], xp, np.cos(xp.sum(0)))
+    assert md2.n == m and md2.covar is md.covar
+
+
 # ---------------------------------------------------------------------------------------
 # a4 dK/dtheta  (test/test_covariance.jl:3-9,84-105)
 # ---------------------------------------------------------------------------------------

@@ -1267,7 +1267,11 @@ hipEvent_t sync_event(gpr_ctx* ctx, size_t i) {
 // Factor the rows [k, k+kw) of the (already updated) trailing matrix: per inner block j:
 // diag factor+inverse, in-place panel TRSM over all columns >= j+jb (MFMA GEMM with
 // U_jj^{-1}), then the update of the remaining rows of this outer panel (K = nb).
+static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
+
 int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  if (ctx->inner_la == 2 && ctx->stream3 && ctx->diag_cus == 0)
+    return factor_panel_bla(ctx, A, n, lda, k, kw);
   // Inner lookahead: after block j's row TRSM, only the NEXT strip (rows of block j+1) is
   // updated on the chain stream; the remaining strips of the panel are updated on stream3
   // beside diag(j+1) and TRSM(j+1).  Strip j+2 must hold that remainder update before the
@@ -1345,6 +1349,100 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   }
   if (e_rest) HIP_TRY(ctx, hipStreamWaitEvent(home, e_rest, 0));  // panel complete on home
   return 0;
+}
+
+// Block lookahead (GPR_INNER_LA=2): the chain stream carries only what the next diagonal
+// block needs -- diag(j), the row TRSM of block j's NEXT nb columns, the update of the next
+// diagonal block -- and the full-width rest of step j (row TRSM of the far columns, update
+// of the far part of the panel) runs on stream3 beside diag(j+1).  The chain waits for step
+// j-1's far update before step j's near TRSM (that update wrote block (j, j+1) and, through
+// the panel rows, block (j+1, j+1)).
+static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  const int nb = ctx->nb;
+  hipStream_t home = ctx->ls, side = ctx->stream3;
+  hipEvent_t e_far = nullptr;  // far update of the previous step (on side)
+  int rc = 0;
+  auto gemm_on = [&](hipStream_t s, GemmArgs& g) {
+    ctx->ls = s;
+    const int r = launch_gemm_tn(ctx, g, TC_PANEL);
+    ctx->ls = home;
+    return r;
+  };
+  for (int j = k; j < k + kw && !rc; j += nb) {
+    const int jb = std::min(nb, n - j);
+    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
+    if ((rc = launch_diag(ctx, A, lda, n, j, wj, 1, 1))) break;
+    if (j + jb >= n) break;
+    const int c1 = j + jb;                  // first column right of block j
+    const int jn = std::min(nb, n - c1);    // width of the next block
+    const int cf = c1 + jn;                 // first far column
+    const int pend = k + kw;                // end of this panel's rows
+    double* row = A + j + (size_t)c1 * lda;  // U_j, columns c1..n
+    hipEvent_t e_d = sync_event(ctx, ctx->ev_next++);
+    HIP_TRY(ctx, hipEventRecord(e_d, home));
+    // ---- chain: near row TRSM (after the previous far update), near diagonal update
+    if (e_far) HIP_TRY(ctx, hipStreamWaitEvent(home, e_far, 0));
+    e_far = nullptr;
+    GemmArgs sn{};
+    sn.P = wj; sn.ldp = nb;
+    sn.Q = row; sn.ldq = lda;
+    sn.C = row; sn.ldc = lda;
+    sn.M = jb; sn.N = jn; sn.K = jb;
+    sn.alpha = 1.0; sn.beta = 0.0;
+    sn.info = ctx->dinfo;
+    if ((rc = gemm_on(home, sn))) break;
+    hipEvent_t e_sn = sync_event(ctx, ctx->ev_next++);
+    HIP_TRY(ctx, hipEventRecord(e_sn, home));
+    if (pend > c1) {
+      GemmArgs un{};
+      un.P = row; un.ldp = lda;
+      un.Q = row; un.ldq = lda;
+      un.C = A + c1 + (size_t)c1 * lda; un.ldc = lda;
+      un.M = jn; un.N = jn; un.K = jb;
+      un.alpha = -1.0; un.beta = 1.0;
+      un.mask_upper = 1;
+      un.info = ctx->dinfo;
+      if ((rc = gemm_on(home, un))) break;
+    }
+    if (cf >= n) continue;  // no far columns: nothing for the side stream
+    // ---- side: far row TRSM, then the far update of the panel rows below block j
+    HIP_TRY(ctx, hipStreamWaitEvent(side, e_d, 0));
+    GemmArgs sf{};
+    sf.P = wj; sf.ldp = nb;
+    sf.Q = A + j + (size_t)cf * lda; sf.ldq = lda;
+    sf.C = A + j + (size_t)cf * lda; sf.ldc = lda;
+    sf.M = jb; sf.N = n - cf; sf.K = jb;
+    sf.alpha = 1.0; sf.beta = 0.0;
+    sf.info = ctx->dinfo;
+    if ((rc = gemm_on(side, sf))) break;
+    if (pend > c1) {
+      HIP_TRY(ctx, hipStreamWaitEvent(side, e_sn, 0));
+      GemmArgs fi{};  // rows of block j+1, far columns
+      fi.P = row; fi.ldp = lda;
+      fi.Q = A + j + (size_t)cf * lda; fi.ldq = lda;
+      fi.C = A + c1 + (size_t)cf * lda; fi.ldc = lda;
+      fi.M = jn; fi.N = n - cf; fi.K = jb;
+      fi.alpha = -1.0; fi.beta = 1.0;
+      fi.info = ctx->dinfo;
+      if ((rc = gemm_on(side, fi))) break;
+      if (pend > cf) {  // the remaining panel rows, far columns (upper part)
+        GemmArgs fr{};
+        fr.P = A + j + (size_t)cf * lda; fr.ldp = lda;
+        fr.Q = fr.P; fr.ldq = lda;
+        fr.C = A + cf + (size_t)cf * lda; fr.ldc = lda;
+        fr.M = pend - cf; fr.N = n - cf; fr.K = jb;
+        fr.alpha = -1.0; fr.beta = 1.0;
+        fr.mask_upper = 1;
+        fr.info = ctx->dinfo;
+        if ((rc = gemm_on(side, fr))) break;
+      }
+    }
+    e_far = sync_event(ctx, ctx->ev_next++);
+    HIP_TRY(ctx, hipEventRecord(e_far, side));
+  }
+  ctx->ls = home;
+  if (e_far) HIP_TRY(ctx, hipStreamWaitEvent(home, e_far, 0));  // panel complete on home
+  return rc;
 }
 
 // All outer-panel square inverses U_sq^{-1} of a finished factor in one launch: grid

@@ -160,6 +160,13 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
   if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);
   if (const char* e = getenv("GPR_INNER_LA")) ctx->inner_la = atoi(e);
+  // Concurrent child contexts of cv_batch / integrate_noise: each drives its own stream, so
+  // by default no more of them than the process has hardware queues (GPU_MAX_HW_QUEUES,
+  // HIP's default 4); more only multiplex onto the same queues.
+  if (const char* e = getenv("GPU_MAX_HW_QUEUES")) {
+    const int q = atoi(e);
+    if (q > 0) ctx->cv_streams = std::min(ctx->cv_streams, q);
+  }
   if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
   // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is

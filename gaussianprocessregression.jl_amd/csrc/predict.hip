@@ -422,7 +422,18 @@ static int ensure_children(gpr_ctx* ctx, int nsub) {
   return 0;
 }
 
-// run body(child t) for t < nsub on host threads; first info > 0, else first error
+// Cap the number of child contexts so their workspaces (bytes_each, allocated in each child's
+// dbig) take at most half of the device memory free right now; at least one child.
+static int cap_children_by_memory(int nsub, size_t bytes_each) {
+  size_t fr = 0, tot = 0;
+  if (nsub <= 1 || bytes_each == 0 || hipMemGetInfo(&fr, &tot) != hipSuccess) return nsub;
+  const size_t fit = (fr / 2) / bytes_each;
+  return (int)std::max<size_t>(1, std::min<size_t>((size_t)nsub, fit));
+}
+
+// run body(child t) for t < nsub on host threads; first info > 0, else first error.  Each
+// child's workspace (dbig) is released after the batch, so the extra device memory lives
+// only as long as the call (the children's streams and small buffers stay for reuse).
 static int run_children(gpr_ctx* ctx, int nsub, const std::function<int(gpr_ctx*, int)>& body) {
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // inputs written on the parent stream
   std::vector<int> rcs(nsub, 0);
@@ -433,6 +444,17 @@ static int run_children(gpr_ctx* ctx, int nsub, const std::function<int(gpr_ctx*
       rcs[t] = body(ctx->cv_sub[t], t);
     });
   for (auto& x : th) x.join();
+  for (int t = 0; t < nsub; ++t) {
+    gpr_ctx* c = ctx->cv_sub[t];
+    if (c && c->dbig) {
+      hipStreamSynchronize(c->stream);
+      hipFree(c->dbig);
+      c->dbig = nullptr;
+      c->big_cap = 0;
+      c->fac_valid = false;  // cached factor data were keyed on pointers into dbig
+      c->sqinv_nb2 = 0;
+    }
+  }
   for (int t = 0; t < nsub; ++t)
     if (rcs[t] > 0) return rcs[t];
   for (int t = 0; t < nsub; ++t)
@@ -530,6 +552,12 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   // folds run concurrently, one child context (own streams, own workspace) per host thread.
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), nfold);
   if (ntrn > 8192) nsub = 1;
+  {  // per-child workspace of cv_folds: K, Sigma_p, inputs/outputs and indices of its folds
+    const size_t per = ((size_t)ntrn * ntrn + (size_t)ntst * ntst +
+                        (size_t)(d + 1) * (ntrn + ntst) + 2 * (size_t)ntst +
+                        (size_t)((nfold + nsub - 1) / std::max(nsub, 1)) * (ntrn + ntst + 1)) * 8;
+    nsub = cap_children_by_memory(nsub, per);
+  }
   if (nsub <= 1)
     return cv_folds(ctx, kinds, nk, hp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, 0, 1, cost,
                     eps, lss);
@@ -598,6 +626,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   GPR_TRY(gpr_antideriv_se(ctx, d, hp, dX, n, a, b, k1, &k2));
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);
   if (n > 8192) nsub = 1;
+  nsub = cap_children_by_memory(nsub, ((size_t)n * n + 2 * (size_t)n + 2 * (size_t)ny) * 8);
   if (nsub <= 1) {
     const int rc = integ_noise_cols(ctx, K, n, n, dy, ldy, k1, k2, noise, ny, 0, 1, Iout, var);
     return rc;

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from . import core
-from ._lib import lib
+from ._lib import GprError, PosDefException, lib
 
 __all__ = ["shard_rows", "HipSplitBackend", "split_predict_distributed"]
 
@@ -58,8 +58,16 @@ class HipSplitBackend:
 
     fit():          gpr_fit -> (U, wt) device tensors (U column-major N x N).
     empty_fit():    receive buffers for the broadcast.
+    publish():      order torch's current stream after the context stream, so a collective
+                    (which waits only on the current stream) sends the finished U / wt.
+    receive():      order the context stream after the current stream, so the split
+                    kernels read U / wt only once the collective's copies have landed.
     predict_rows(): gpr_split_predict for grid rows [e_lo, e_hi) into full-layout device
                     buffers (mu: nq x ne tensor = ne x nq column-major; var: ne nq).
+
+    gpr_fit returns once the factorisation's info is known, with the wt solve still queued
+    on the context stream; RCCL runs on its own stream that waits on torch's current stream
+    only -- hence publish()/receive() around every collective on device buffers.
     """
 
     def __init__(self, md: core.GPRModel, eps: float = core.EPS_DEFAULT):
@@ -77,6 +85,12 @@ class HipSplitBackend:
         core._update_predict_cache(core.pc_adapter(pc), self.md, self.eps)
         return pc.Kxx, pc.wt
 
+    def publish(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.ctx.stream)
+
+    def receive(self):
+        self.ctx.stream.wait_stream(torch.cuda.current_stream(self.device))
+
     def predict_rows(self, cm: core.Cmap, U, wt, e_lo: int, e_hi: int, v_lo: int, v_hi: int):
         md, ctx = self.md, self.ctx
         _, ne, nq = cm.shape
@@ -91,6 +105,16 @@ class HipSplitBackend:
                                         core._ptr(mu), core._ptr(var)), "gpr_split_predict")
         ctx.sync()
         return mu, var
+
+
+def _src(group) -> int:
+    return dist.get_global_rank(group, 0) if group is not None else 0
+
+
+def _hook(backend, name: str):
+    f = getattr(backend, name, None)
+    if f is not None:
+        f()
 
 
 def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
@@ -110,17 +134,45 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
     backend = backend or HipSplitBackend(md, eps)
     _, ne, nq = cm.shape
 
-    # 1. factor + weights: rank 0 (broadcast) or every rank (replicate)
-    if fit == "broadcast":
-        if rank == 0:
+    # 1. factor + weights: rank 0 (broadcast) or every rank (replicate).  A failed fit is
+    #    turned into a status every rank sees before any data collective, so all ranks raise
+    #    the same exception instead of the others blocking in a broadcast / all_gather.
+    dev = getattr(backend, "device", None) or torch.device("cpu")
+    U = wt = None
+    err: Optional[BaseException] = None
+    if fit == "replicate" or rank == 0:
+        try:
             U, wt = backend.fit()
-        else:
-            U, wt = backend.empty_fit()
-        src = dist.get_global_rank(group, 0) if group is not None else 0
-        dist.broadcast(U, src, group=group)
-        dist.broadcast(wt, src, group=group)
+            code = 0
+        except PosDefException as e:
+            err, code = e, int(e.info)
+        except Exception as e:  # noqa: BLE001 -- re-raised below, after the status exchange
+            err, code = e, -1
     else:
-        U, wt = backend.fit()
+        code = 0
+    status = torch.tensor([code], dtype=torch.int64, device=dev)
+    if fit == "broadcast":
+        dist.broadcast(status, _src(group), group=group)
+    else:  # any failing rank: report the first failure class (PosDef info > 0 wins)
+        neg = torch.tensor([1 if code < 0 else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(status, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(neg, op=dist.ReduceOp.MAX, group=group)
+        if int(status.item()) == 0 and int(neg.item()) > 0:
+            status.fill_(-1)
+    code_all = int(status.item())
+    if code_all != 0:
+        if err is not None:
+            raise err
+        if code_all > 0:
+            raise PosDefException(code_all)
+        raise GprError("split_predict_distributed: the fit failed on another rank")
+    if fit == "broadcast":
+        if rank != 0:
+            U, wt = backend.empty_fit()
+        _hook(backend, "publish")
+        dist.broadcast(U, _src(group), group=group)
+        dist.broadcast(wt, _src(group), group=group)
+        _hook(backend, "receive")
 
     # 2. this rank's grid rows and the var_range rows inside them
     lo, hi = shard_rows(ne, world, rank)

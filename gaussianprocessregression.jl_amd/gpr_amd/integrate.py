@@ -111,7 +111,14 @@ def _integrate_noise(md: C.GPRModel, hp, a, b, sample_noise, eps: float):
     """integrate(...; sample_noise::Vector) (src/integrate.jl:71-100,149-162): column j of y
     is integrated with K + sample_noise[j] I.  A scalar sample_noise has no variance method
     in the reference (var_integ_impl! reaches inverse_diagonal_update2!(var, lam, P,
-    ::Float64, k1, tmp), which is not defined: MethodError) -- mirrored as TypeError."""
+    ::Float64, k1, tmp), which is not defined: MethodError) -- mirrored as TypeError.
+
+    Divergence (parity unpinned: no reference fixture covers it): the reference diagonalises
+    K once and applies 1 / (lambda + noise_j), so it never throws; here each K + noise_j I is
+    factored by Cholesky.  Both agree whenever K + noise_j I is positive definite (negative
+    noise_j > -lambda_min included); where noise_j <= -lambda_min the reference returns the
+    values of an indefinite solve and this raises PosDefException(info) instead
+    (tests/test_integrate.py::test_integrate_sample_noise_negative)."""
     noise = np.asarray(sample_noise, dtype=np.float64)
     if noise.ndim == 0:
         raise TypeError("integrate(...; sample_noise::Float64): no method "

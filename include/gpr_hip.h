@@ -211,7 +211,9 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  The reference diagonalises K once (LAPACK
  * syevr) and applies (Lambda + noise_j)^{-1}; here each shifted matrix is factored by the
  * MFMA POTRF (same quantities; independent columns run on concurrent child contexts).
- * Returns info > 0 if some K + noise_j I is not positive definite. */
+ * Returns info > 0 if some K + noise_j I is not positive definite.  Divergence from the
+ * reference (which diagonalises K and never throws): for noise_j <= -lambda_min(K) the
+ * reference returns an indefinite solve, this returns info > 0 (PosDefException). */
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                         const double* dX, int n, const double* dy, int ny, int ldy,
                         const double* a, const double* b, const double* noise, double eps,

@@ -119,6 +119,58 @@ def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit)
         np.testing.assert_allclose(var, var_o, rtol=1e-12, atol=1e-14)
 
 
+class FailingBackend(OracleBackend):
+    """fit() raises on the ranks listed in `fail` (PosDefException(info) or a generic error)."""
+
+    def __init__(self, *a, fail=(), info=7, **kw):
+        super().__init__(*a, **kw)
+        self.fail, self.info = fail, info
+
+    def fit(self):
+        if dist.get_rank() in self.fail:
+            if self.info > 0:
+                from gpr_amd._lib import PosDefException
+                raise PosDefException(self.info)
+            raise RuntimeError("simulated HIP failure")
+        return super().fit()
+
+
+def _fail_worker(rank, world, port, out, fit, fail, info):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kinds, hp, x, y, xe, xq = _problem(ne=5, nq=3)
+        be = FailingBackend(kinds, hp, x, y, fail=fail, info=info)
+        try:
+            gd.split_predict_distributed(None, _Cmap(xe, xq), backend=be, fit=fit)
+            res = "ok"
+        except Exception as e:  # noqa: BLE001
+            res = f"{type(e).__name__}:{getattr(e, 'info', '')}"
+        with open(os.path.join(out, f"r{rank}.txt"), "w") as f:
+            f.write(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fit,fail,info,expect", [
+    ("broadcast", (0,), 7, "PosDefException:7"),    # rank 0's PosDef reaches every rank
+    ("broadcast", (0,), 0, None),                    # generic failure: no rank hangs
+    ("replicate", (1,), 3, "PosDefException:3"),    # one replica fails: all raise
+])
+def test_split_predict_distributed_fit_failure(tmp_path, fit, fail, info, expect):
+    """A failed fit raises on EVERY rank (the other ranks used to block in the
+    broadcast).  mp.spawn with join=True would hang here if any rank blocked."""
+    world = 3
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path), fit, fail, info),
+             nprocs=world, join=True)
+    res = [open(tmp_path / f"r{r}.txt").read() for r in range(world)]
+    assert all(r != "ok" for r in res), res
+    if expect is not None:
+        assert all(r == expect for r in res), res
+    else:
+        assert res[0].startswith("RuntimeError") and all(r.startswith("GprError") for r in res[1:])
+
+
 def test_shard_rows_partition():
     for n in range(0, 40):
         for world in range(1, 9):
@@ -158,3 +210,39 @@ def test_split_predict_distributed_hip_single_rank():
         np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
     finally:
         dist.destroy_process_group()
+
+
+def _hip_gloo_worker(rank, world, port, out, fit):
+    """Two ranks on ONE GPU over gloo with device tensors: the HIP backend's stream ordering
+    around the collectives (gpr_fit leaves the wt solve queued on the context stream; the
+    collectives order only against torch's current stream)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gpr_amd as G
+        kinds, hp, x, y, xe, xq = _problem(ne=9, nq=40, ns=4096, d=6, seed=11)
+        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+        cm = G.Cmap("+", xe, xq)
+        for it in range(3):
+            mu, var = gd.split_predict_distributed(md, cm, var_range=(1, 9), fit=fit)
+            np.save(os.path.join(out, f"mu{rank}_{it}.npy"), mu)
+            np.save(os.path.join(out, f"var{rank}_{it}.npy"), var)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fit", ["broadcast", "replicate"])
+def test_split_predict_distributed_hip_two_ranks(tmp_path, fit):
+    """world = 2 on the HIP backend (both ranks on cuda:0, gloo carrying device tensors),
+    N = 4096 so the fit's queued solve and the broadcast overlap if unordered: every rank's
+    result equals the single-process split predict (rtol 1e-12; a race shows as O(1) errors)."""
+    G = pytest.importorskip("gpr_amd")
+    mp.spawn(_hip_gloo_worker, args=(2, _free_port(), str(tmp_path), fit), nprocs=2, join=True)
+    kinds, hp, x, y, xe, xq = _problem(ne=9, nq=40, ns=4096, d=6, seed=11)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    mu1, var1 = G.predict(md, G.Cmap("+", xe, xq), diagonal_var=True, var_range=(1, 9))
+    for r in range(2):
+        for it in range(3):
+            np.testing.assert_allclose(np.load(tmp_path / f"mu{r}_{it}.npy"), mu1, rtol=1e-12, atol=1e-14)
+            np.testing.assert_allclose(np.load(tmp_path / f"var{r}_{it}.npy"), var1, rtol=1e-12, atol=1e-14)

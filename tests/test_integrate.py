@@ -140,6 +140,30 @@ def test_integrate_sample_noise_vs_oracle(name, dim, n, ne):
 
 
 @pytest.mark.gpu
+def test_integrate_sample_noise_negative():
+    """Boundary of the documented divergence: a negative noise that keeps
+    K + noise I positive definite matches the oracle's eigen path (src/integrate.jl:71-100);
+    one below -lambda_min raises PosDefException where the reference's eigen path would
+    return an indefinite solve."""
+    dim, n = 3, 200
+    kinds = [O.SE, O.WN]
+    rng = np.random.default_rng(5)
+    x = rng.random((dim, n))
+    Y = rng.random((n, 2))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)   # lambda_min(K) >= 0.05^2
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    lam_min = np.linalg.eigvalsh(O.kernel(kinds, hp, x)).min()
+    noise = np.array([-0.5 * lam_min, 0.0])
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I, Io, rtol=1e-7)
+    np.testing.assert_allclose(v, vo, rtol=1e-6, atol=1e-10 * O.antideriv2_se(hp, a, b))
+    with pytest.raises(G.PosDefException):
+        G.integrate(md, a, b, sample_noise=np.array([1e-3, -2.0 * lam_min - 1.0]))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dim,n,k", [(1, 100, 100), (2, 200, 300), (4, 300, 200)])
 def test_integrate_zero_noise_reference(dim, n, k):
     """test/test_integrate.jl:113-126 (random hp as GPRModel(SquaredExp(), x, y))."""

@@ -50,6 +50,7 @@ struct gpr_ctx {
   hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
   hipStream_t stream2 = nullptr;  // lookahead panel stream (GEMMs of the panel chain)
   hipStream_t stream3 = nullptr;  // inner lookahead: panel-update remainder beside the chain
+  int panel_mode = 0;             // 2: square chain + left-looking strip (GPR_PANEL)
   int inner_la = 0;               // split the panel inner update (GPR_INNER_LA=1; no gain measured)
   hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
   hipStream_t smain = nullptr;    // big trailing updates: CU mask = all but the reserved CUs

@@ -487,6 +487,127 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_pipe16_kernel(GemmK a) { gemm_
 __global__ __launch_bounds__(256, 2) void gemm_tn_pipe8_kernel(GemmK a) { gemm_tn_pipe_body<8, true>(a); }
 __global__ __launch_bounds__(256, 2) void gemm_tn_pipe8z_kernel(GemmK a) { gemm_tn_pipe_body<8, false>(a); }
 
+// ---- narrow-tile variant for short-K launches with few 128x128 tiles -------------------
+// The latency-bound panel chain of the factorisation issues K <= 128..256 GEMMs with one
+// or a few 128-row tile rows (row TRSM M = 128, in-panel updates): at 128 x 128 tiles such a
+// launch occupies a fraction of the CUs and each tile's K loop runs at one CU's MFMA rate
+// (128 x 128 x 128 = 13.7 us at 0.31 TF/s per CU).  A 128 x 32 tile spreads the same work
+// over 4x the CUs: wave w owns rows 32w..32w+31 and all 32 columns (2 x 2 blocks of
+// 16 x 16, 128 MFMAs per K = 128).  Each tile still covers whole 128-row spans of K, so the
+// in-place row TRSM (C = Q, M = 128) stays safe: a tile reads all K rows of its columns
+// before its epilogue writes them.  Register-prefetched, double-buffered LDS stages of 16 k.
+constexpr int NTN = 32;
+__global__ __launch_bounds__(256, 4) void gemm_tn_narrow_kernel(GemmK a) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const GemmArgs& g = a.g;
+  if (g.info && *g.info != 0) return;
+  __shared__ double Ps[2][TM * LDT];
+  __shared__ double Qs[2][NTN * LDT];
+  const int bid = blockIdx.x;
+  const int tm = bid % a.tiles_m, tn = bid / a.tiles_m;
+  if (tn >= a.tiles_n) return;
+  const int m0 = tm * TM, n0 = tn * NTN;
+  if ((g.upper || g.mask_upper) && m0 > n0 + NTN - 1 + g.mask_off) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kbeg = g.kfrom_n ? n0 : 0;
+  const int kend = g.kend_from_m ? min(g.K, m0 + TM) : g.K;
+  const int nst = kend > kbeg ? (kend - kbeg + TK - 1) / TK : 0;
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  // stage loads: P 128 rows x 8 k-pairs (4 per thread), Q 32 rows x 8 k-pairs (1 per thread);
+  // clamped addresses, out-of-range pairs zeroed at the LDS store (K even: pairs whole)
+  d2 vp[4], vq;
+  auto gload = [&](int st) {
+    const int k0 = kbeg + st * TK;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int idx = tid + 256 * r;
+      const int row = idx >> 3, k = k0 + 2 * (idx & 7);
+      const int kc = k < kend ? k : kbeg;
+      vp[r] = *reinterpret_cast<const d2*>(g.P + (size_t)kc + (size_t)min(m0 + row, g.M - 1) * g.ldp);
+    }
+    const int row = tid >> 3, k = k0 + 2 * (tid & 7);
+    const int kc = k < kend ? k : kbeg;
+    vq = *reinterpret_cast<const d2*>(g.Q + (size_t)kc + (size_t)min(n0 + row, g.N - 1) * g.ldq);
+  };
+  auto lstore = [&](int buf, int st) {
+    const int k0 = kbeg + st * TK;
+    const d2 z = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int idx = tid + 256 * r;
+      const int row = idx >> 3, kp = idx & 7;
+      *reinterpret_cast<d2*>(&Ps[buf][lds_idx(row, kp)]) = (k0 + 2 * kp < kend) ? vp[r] : z;
+    }
+    const int row = tid >> 3, kp = tid & 7;
+    *reinterpret_cast<d2*>(&Qs[buf][lds_idx(row, kp)]) = (k0 + 2 * kp < kend) ? vq : z;
+  };
+  if (nst > 0) {
+    gload(0);
+    lstore(0, 0);
+    __syncthreads();
+  }
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) gload(st + 1);
+    const double* ps = Ps[buf];
+    const double* qs = Qs[buf];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int ch = (lane >> 4) + 4 * p;
+      d2 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const d2*>(&qs[lds_idx(i * 16 + (lane & 15), ch)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bf[j] = *reinterpret_cast<const d2*>(&ps[lds_idx(w * 32 + j * 16 + (lane & 15), ch)]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i][h], bf[j][h], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < nst) lstore(buf ^ 1, st + 1);
+    __syncthreads();
+  }
+  // epilogue: D lane l reg r = (n = (l >> 4) + 4r, m = l & 15) of each 16 x 16 block; all C
+  // loads first, then the stores
+  const bool has_beta = g.beta != 0.0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + i * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = m0 + w * 32 + j * 16 + (lane & 15);
+        const bool in = m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n + g.mask_off);
+        double v = g.alpha * acc[i][j][r];
+        if (has_beta) v = v + g.beta * (in ? g.C[(size_t)m + (size_t)n * g.ldc] : 0.0);
+        acc[i][j][r] = v;
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + i * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = m0 + w * 32 + j * 16 + (lane & 15);
+        if (m < g.M && n < g.N && (!(g.upper || g.mask_upper) || m <= n + g.mask_off))
+          g.C[(size_t)m + (size_t)n * g.ldc] = acc[i][j][r];
+      }
+    }
+}
+
 }  // namespace
 
 // GPR_GEMM_PIPE: 1 = the 1-WG/CU variant, 2 (default) = the 2-WG/CU variant (faster at every
@@ -554,6 +675,18 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
                    !vec_off();
   // pipelined variants need K - kbeg to be a whole number of stages (kbeg is 0 or a
   // multiple of TN); long K goes to the one-workgroup-per-CU variant
+  // few 128 x 128 tiles at short K: the narrow-tile kernel spreads them over 4x the CUs
+  // (GPR_GEMM_NARROW = max 128x128 tiles for it, default 384; 0 disables)
+  static const int narrow_max = getenv("GPR_GEMM_NARROW") ? atoi(getenv("GPR_GEMM_NARROW")) : 384;
+  if (vec && !g.occ1 && !g.E && !g.norm_out && g.K <= 256 && nblk <= narrow_max &&
+      !(g.upper && g.kfrom_n)) {
+    GemmK an = a;
+    an.tiles_n = (g.N + NTN - 1) / NTN;
+    const long long nb_n = (long long)an.tiles_m * an.tiles_n;
+    gemm_tn_narrow_kernel<<<(unsigned)nb_n, 256, 0, ctx->ls>>>(an);
+    LAUNCH_CHECK(ctx);
+    return 0;
+  }
   const int pipe_mode = pipe_off() ? 0 : pipe_env();
   const bool pipe = vec && (g.K % TK) == 0 && !g.occ1 && pipe_mode != 0;
   const bool long_k = pipe_mode == 1 || (pipe_mode == 3 && g.K >= 2048);

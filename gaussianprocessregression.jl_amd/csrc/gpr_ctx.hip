@@ -167,6 +167,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     const int q = atoi(e);
     if (q > 0) ctx->cv_streams = std::min(ctx->cv_streams, q);
   }
+  if (const char* e = getenv("GPR_PANEL")) ctx->panel_mode = atoi(e);
   if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
   // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is

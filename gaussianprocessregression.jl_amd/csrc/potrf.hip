@@ -1269,7 +1269,11 @@ hipEvent_t sync_event(gpr_ctx* ctx, size_t i) {
 // U_jj^{-1}), then the update of the remaining rows of this outer panel (K = nb).
 static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
 
+static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
+
 int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  if (ctx->panel_mode == 2 && ctx->stream3 && ctx->diag_cus == 0 && !ctx->inner_la)
+    return factor_panel_ll(ctx, A, n, lda, k, kw);
   if (ctx->inner_la == 2 && ctx->stream3 && ctx->diag_cus == 0)
     return factor_panel_bla(ctx, A, n, lda, k, kw);
   // Inner lookahead: after block j's row TRSM, only the NEXT strip (rows of block j+1) is
@@ -1349,6 +1353,89 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   }
   if (e_rest) HIP_TRY(ctx, hipStreamWaitEvent(home, e_rest, 0));  // panel complete on home
   return 0;
+}
+
+// Square chain + left-looking strip (GPR_PANEL=2).  The inner blocks of the outer panel's
+// kw x kw diagonal square are factored on the chain stream with updates restricted to the
+// square (diag(j); U(j, square) = W_j^T A(j, square); A(square rows > j) -= U(j)^T U(j)):
+// the chain's GEMMs have at most 7 x 7 tiles, so they neither wait long for CU slots nor
+// take many from the trailing SYRK.  The strip right of the square (rows [k, k+kw), columns
+// [k+kw, n)) is solved block row by block row on the side stream, left-looking:
+//   B_i -= U(k:k+128i, i)^T R_{0:i}   (M = 128, N = n-k-kw, K = 128 i, beta = 1)
+//   R_i  = W_i^T B_i                  (in place, K = 128)
+// Step i needs only W_i and the square's column block i, both final once diag(i) ran, so the
+// strip trails the chain by one step instead of widening every chain GEMM to n - j columns
+// (whose K = 128 read-modify-write of up to 896 x n elements per step was the bulk of the
+// lookahead stream's time).  Same arithmetic as the right-looking panel up to summation order.
+static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  const int nb = ctx->nb;
+  hipStream_t home = ctx->ls, side = ctx->stream3;
+  const int kend = k + kw, nrest = n - kend;
+  int rc = 0;
+  auto gemm_on = [&](hipStream_t st, GemmArgs& g) {
+    ctx->ls = st;
+    const int r = launch_gemm_tn(ctx, g, TC_PANEL);
+    ctx->ls = home;
+    return r;
+  };
+  bool side_used = false;
+  for (int j = k; j < kend && !rc; j += nb) {
+    const int jb = std::min(nb, n - j);
+    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
+    if ((rc = launch_diag(ctx, A, lda, n, j, wj, 1, 1))) break;
+    if (nrest > 0) {  // strip step for block j on the side stream, after diag(j)
+      hipEvent_t ed = sync_event(ctx, ctx->ev_next++);
+      HIP_TRY(ctx, hipEventRecord(ed, home));
+      HIP_TRY(ctx, hipStreamWaitEvent(side, ed, 0));
+      side_used = true;
+      if (j > k) {
+        GemmArgs u{};
+        u.P = A + k + (size_t)j * lda; u.ldp = lda;          // U(k:j, block j)
+        u.Q = A + k + (size_t)kend * lda; u.ldq = lda;       // R_{0:i}
+        u.C = A + j + (size_t)kend * lda; u.ldc = lda;       // B_i
+        u.M = jb; u.N = nrest; u.K = j - k;
+        u.alpha = -1.0; u.beta = 1.0;
+        u.info = ctx->dinfo;
+        if ((rc = gemm_on(side, u))) break;
+      }
+      GemmArgs t{};
+      t.P = wj; t.ldp = nb;
+      t.Q = A + j + (size_t)kend * lda; t.ldq = lda;
+      t.C = A + j + (size_t)kend * lda; t.ldc = lda;
+      t.M = jb; t.N = nrest; t.K = jb;
+      t.alpha = 1.0; t.beta = 0.0;
+      t.info = ctx->dinfo;
+      if ((rc = gemm_on(side, t))) break;
+    }
+    const int c1 = j + jb;
+    if (c1 >= kend) break;
+    // chain: row j inside the square, then the square's rows below j
+    double* row = A + j + (size_t)c1 * lda;
+    GemmArgs g{};
+    g.P = wj; g.ldp = nb;
+    g.Q = row; g.ldq = lda;
+    g.C = row; g.ldc = lda;
+    g.M = jb; g.N = kend - c1; g.K = jb;
+    g.alpha = 1.0; g.beta = 0.0;
+    g.info = ctx->dinfo;
+    if ((rc = launch_gemm_tn(ctx, g, TC_PANEL))) break;
+    GemmArgs u{};
+    u.P = row; u.ldp = lda;
+    u.Q = row; u.ldq = lda;
+    u.C = A + c1 + (size_t)c1 * lda; u.ldc = lda;
+    u.M = kend - c1; u.N = kend - c1; u.K = jb;
+    u.alpha = -1.0; u.beta = 1.0;
+    u.upper = 1;
+    u.info = ctx->dinfo;
+    if ((rc = launch_gemm_tn(ctx, u, TC_PANEL))) break;
+  }
+  ctx->ls = home;
+  if (side_used) {  // panel complete on home
+    hipEvent_t es = sync_event(ctx, ctx->ev_next++);
+    HIP_TRY(ctx, hipEventRecord(es, side));
+    HIP_TRY(ctx, hipStreamWaitEvent(home, es, 0));
+  }
+  return rc;
 }
 
 // Block lookahead (GPR_INNER_LA=2): the chain stream carries only what the next diagonal

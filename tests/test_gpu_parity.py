@@ -197,14 +197,21 @@ def test_potrf_upper(n, nb):
     assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
 
 
-@pytest.mark.parametrize("panel_sq", ["1", "0", "la2"])
+def _panel_env(monkeypatch, mode):
+    """Panel schedule under test: "0" per-block full-width panel, "1" square-panel kernel,
+    "la2" block lookahead, "ll" square chain + left-looking strip (GPR_PANEL=2)."""
+    monkeypatch.setenv("GPR_PANEL_SQ", mode if mode in ("0", "1") else "0")
+    monkeypatch.setenv("GPR_INNER_LA", "2" if mode == "la2" else "0")
+    monkeypatch.setenv("GPR_PANEL", "2" if mode == "ll" else "0")
+
+
+@pytest.mark.parametrize("panel_sq", ["1", "0", "la2", "ll"])
 @pytest.mark.parametrize("n,nb2", [(300, 256), (1000, 256), (1300, 512), (2600, 1024), (1024, 1024),
-                                   (1025, 1024), (777, 2048)])
+                                   (1025, 1024), (777, 2048), (3000, 384)])
 def test_potrf_outer_panels(n, nb2, panel_sq, monkeypatch):
     """Two-level factorisation across outer-panel boundaries (square-panel kernel + rest
     GEMM, and the per-block path), ragged last panels and tiles."""
-    monkeypatch.setenv("GPR_PANEL_SQ", "0" if panel_sq == "la2" else panel_sq)
-    monkeypatch.setenv("GPR_INNER_LA", "2" if panel_sq == "la2" else "0")
+    _panel_env(monkeypatch, panel_sq)
     ctx = G.Context(0)
     assert G._lib.lib.gpr_set_outer_block(ctx.h, nb2) == 0
     A = _spd(n, seed=n + nb2)
@@ -222,11 +229,10 @@ def test_potrf_outer_panels(n, nb2, panel_sq, monkeypatch):
     assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
 
 
-@pytest.mark.parametrize("panel_sq", ["1", "0", "la2"])
+@pytest.mark.parametrize("panel_sq", ["1", "0", "la2", "ll"])
 @pytest.mark.parametrize("j", [0, 255, 256, 700, 1299])
 def test_potrf_not_posdef_info_later_panels(j, panel_sq, monkeypatch):
-    monkeypatch.setenv("GPR_PANEL_SQ", "0" if panel_sq == "la2" else panel_sq)
-    monkeypatch.setenv("GPR_INNER_LA", "2" if panel_sq == "la2" else "0")
+    _panel_env(monkeypatch, panel_sq)
     ctx = G.Context(0)
     assert G._lib.lib.gpr_set_outer_block(ctx.h, 256) == 0
     A = _spd(1300, seed=2)

@@ -50,7 +50,9 @@ struct gpr_ctx {
   hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
   hipStream_t stream2 = nullptr;  // lookahead panel stream (GEMMs of the panel chain)
   hipStream_t stream3 = nullptr;  // inner lookahead: panel-update remainder beside the chain
-  int panel_mode = 0;             // 2: square chain + left-looking strip (GPR_PANEL)
+  int panel_mode = 0;             // 2: square chain + left-looking strip, 3: + inverse strip
+                                  // for strips >= inv_strip_min columns (GPR_PANEL)
+  int inv_strip_min = 12288;      // GPR_INV_STRIP_MIN
   int inner_la = 0;               // split the panel inner update (GPR_INNER_LA=1; no gain measured)
   hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
   hipStream_t smain = nullptr;    // big trailing updates: CU mask = all but the reserved CUs
@@ -58,7 +60,9 @@ struct gpr_ctx {
   hipStream_t ssq = nullptr;      // square inverses of finished outer panels (fused solves)
   // gpr_fit_predict: 0 = factor, then solve (default); 1 / 2 = solve inside the factorisation
   // on its own stream / on the main stream (GPR_FUSED_RHS; measured slower at C3: 347 vs 334 ms)
-  int fused_rhs = 0;
+  int fused_rhs = -1;             // gpr_fit_predict: -1 auto (fused, mode 2, for n <=
+                                  // fused_rhs_nmax), 0 off, 1/2 forced (GPR_FUSED_RHS)
+  int fused_rhs_nmax = 16384;     // GPR_FUSED_RHS_NMAX
   int fuse_y = 0;
   int fuse_kinv = 1;              // gpr_fit_kinv: Z = U^{-T} solved inside the factorisation                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
@@ -195,6 +199,7 @@ struct RhsSpec {
   int nrhs;
   int ldb;
   int lower_rhs;
+  int mode;  // 1: own stream (srhs) beside the trailing updates; 2: main stream after each SYRK
 };
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
                const RhsSpec* rhs = nullptr);

@@ -154,6 +154,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     return GPR_E_HIP;
   }
   if (const char* e = getenv("GPR_FUSED_RHS")) ctx->fused_rhs = atoi(e);
+  if (const char* e = getenv("GPR_FUSED_RHS_NMAX")) ctx->fused_rhs_nmax = atoi(e);
   if (const char* e = getenv("GPR_FUSE_Y")) ctx->fuse_y = atoi(e);
   if (const char* e = getenv("GPR_FUSE_KINV")) ctx->fuse_kinv = atoi(e);
   if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
@@ -168,6 +169,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     if (q > 0) ctx->cv_streams = std::min(ctx->cv_streams, q);
   }
   if (const char* e = getenv("GPR_PANEL")) ctx->panel_mode = atoi(e);
+  if (const char* e = getenv("GPR_INV_STRIP_MIN")) ctx->inv_strip_min = atoi(e);
   if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
   // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is

@@ -1271,7 +1271,12 @@ static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int 
 
 static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
 
+static int factor_panel_inv(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
+
 int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  if (ctx->panel_mode == 3 && ctx->nb == 128 && ctx->diag_cus == 0 && !ctx->inner_la &&
+      n - k - kw >= std::max(1, ctx->inv_strip_min) && ctx->nb2 <= 2048 && ctx->nb2 >= 128)
+    return factor_panel_inv(ctx, A, n, lda, k, kw);
   if (ctx->panel_mode == 2 && ctx->stream3 && ctx->diag_cus == 0 && !ctx->inner_la)
     return factor_panel_ll(ctx, A, n, lda, k, kw);
   if (ctx->inner_la == 2 && ctx->stream3 && ctx->diag_cus == 0)
@@ -1436,6 +1441,74 @@ static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int k
     HIP_TRY(ctx, hipStreamWaitEvent(home, es, 0));
   }
   return rc;
+}
+
+// Square chain + inverse strip (GPR_PANEL=3, outer panels whose strip is at least
+// ctx->inv_strip_min columns wide).  The kw x kw diagonal square is factored on the chain
+// with updates restricted to the square (as factor_panel_ll); then U_sq^{-1} is formed from
+// the square and its block inverses (sqinv_kernel, one workgroup per block column) and the
+// strip right of the square is ONE K = kw GEMM, X = U_sq^{-T} A(k:k+kw, k+kw:n), with the
+// K range cut at each tile's diagonal (out of place, strided copy back).  The per-block
+// form spends the strip's kw^2 (n - k - kw) flops in K = 128 GEMMs that read-modify-write up
+// to 896 x (n - j) elements per step; beside the trailing SYRK those take CU time out of
+// proportion to their flops.  The inverse costs a latency of ~0.5 ms per panel (hidden
+// behind a wide trailing SYRK), so narrow strips keep the per-block form.
+__global__ void sqinv_kernel(const double* __restrict__ U, size_t ldu, int n, int nb2, int p0,
+                             const double* __restrict__ winv, double* __restrict__ sqinv);
+
+static int factor_panel_inv(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  constexpr int NB = 128;
+  const int nb = ctx->nb, nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
+  const int kend = k + kw, nrest = n - kend;
+  GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap,
+                     (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));
+  for (int j = k; j < kend; j += nb) {
+    const int jb = std::min(nb, n - j);
+    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
+    GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
+    const int c1 = j + jb;
+    if (c1 >= kend) break;
+    double* row = A + j + (size_t)c1 * lda;
+    GemmArgs g{};
+    g.P = wj; g.ldp = nb;
+    g.Q = row; g.ldq = lda;
+    g.C = row; g.ldc = lda;
+    g.M = jb; g.N = kend - c1; g.K = jb;
+    g.alpha = 1.0; g.beta = 0.0;
+    g.info = ctx->dinfo;
+    GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
+    GemmArgs u{};
+    u.P = row; u.ldp = lda;
+    u.Q = row; u.ldq = lda;
+    u.C = A + c1 + (size_t)c1 * lda; u.ldc = lda;
+    u.M = kend - c1; u.N = kend - c1; u.K = jb;
+    u.alpha = -1.0; u.beta = 1.0;
+    u.upper = 1;
+    u.info = ctx->dinfo;
+    GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
+  }
+  double* sq = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2;
+  {
+    TimerScope ts(ctx, TC_PANEL, 0.0);
+    sqinv_kernel<<<dim3(1, (kw + NB - 1) / NB), 256, 0, ctx->ls>>>(A, (size_t)lda, n, nb2,
+                                                                   k / nb2, ctx->winv,
+                                                                   ctx->dsqinv);
+    LAUNCH_CHECK(ctx);
+  }
+  GPR_TRY(ensure_buf(ctx, &ctx->dpanel, &ctx->panel_cap, (size_t)kw * nrest));
+  GemmArgs g{};
+  g.P = sq; g.ldp = kw;                                  // U_sq^{-1}, upper triangular
+  g.Q = A + k + (size_t)kend * lda; g.ldq = lda;         // rows [k, kend) right of the square
+  g.C = ctx->dpanel; g.ldc = kw;                         // out of place: tiles share Q columns
+  g.M = kw; g.N = nrest; g.K = kw;
+  g.alpha = 1.0; g.beta = 0.0;
+  g.kend_from_m = 1;
+  g.info = ctx->dinfo;
+  GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
+  HIP_TRY(ctx, hipMemcpy2DAsync(A + k + (size_t)kend * lda, sizeof(double) * lda, ctx->dpanel,
+                                sizeof(double) * kw, sizeof(double) * kw, nrest,
+                                hipMemcpyDeviceToDevice, ctx->ls));
+  return 0;
 }
 
 // Block lookahead (GPR_INNER_LA=2): the chain stream carries only what the next diagonal
@@ -1722,7 +1795,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   if (s0 != user) HIP_TRY(ctx, hipStreamWaitEvent(s0, e0, 0));
   // fused_rhs 1: right-hand sides on their own stream (srhs); 2: on the main stream after each
   // trailing SYRK (serialised with the big updates, overlapping only the panel chain)
-  hipStream_t sr = !rhs ? nullptr : (ctx->fused_rhs == 2 ? s0 : ctx->srhs);
+  hipStream_t sr = !rhs ? nullptr : (rhs->mode == 2 ? s0 : ctx->srhs);
   if (sr && sr != s0) HIP_TRY(ctx, hipStreamWaitEvent(sr, e0, 0));
   ctx->ls = s1;
   const bool sqp = ctx->panel_sq && nb == 128 && nb2 <= 2048;

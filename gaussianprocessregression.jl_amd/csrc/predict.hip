@@ -196,7 +196,7 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, co
   int hinfo = 0;
   if (ctx->fuse_y) {
     // z = U^{-T} y solved inside the factorisation (side stream), then the backward sweep
-    RhsSpec rhs{dalpha, nrhs, n, 0};
+    RhsSpec rhs{dalpha, nrhs, n, 0, ctx->fused_rhs == 2 ? 2 : 1};
     GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
     if (info) *info = hinfo;
     if (hinfo != 0) return hinfo;
@@ -266,7 +266,7 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   int hinfo = 0;
   // Z = U^{-T} (identity right-hand side, lower triangular) solved in the factorisation's
   // lookahead bubbles (GPR_FUSE_KINV=0: after it, as gpr_potri_upper)
-  RhsSpec rhs{Z, n, n, 1};
+  RhsSpec rhs{Z, n, n, 1, ctx->fused_rhs == 2 ? 2 : 1};
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, ctx->fuse_kinv ? &rhs : nullptr));
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
@@ -285,7 +285,12 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
     return set_err(ctx, GPR_E_ARG, "bad args");
   if (mode != GPR_PREDICT_MEAN && !dvar) return set_err(ctx, GPR_E_ARG, "dvar is NULL");
   if (mode == GPR_PREDICT_FULL && ldv < m) return set_err(ctx, GPR_E_ARG, "ldv < m");
-  if (mode == GPR_PREDICT_MEAN || !ctx->fused_rhs) {
+  // Fused (solve [K(x, xp) | y] inside the factorisation) pays where the factorisation is
+  // chain-bound and leaves the GPU idle: measured C2 (n = 8192, np = 8192) 21.0 -> 18.9 ms,
+  // n = 16384 70.9 -> 67.3; at n = 32768 the trailing SYRKs fill the GPU and the fused
+  // solve slows them (r01: 347 vs 334 ms), so auto fuses only up to fused_rhs_nmax.
+  const int fmode = ctx->fused_rhs < 0 ? (n <= ctx->fused_rhs_nmax ? 2 : 0) : ctx->fused_rhs;
+  if (mode == GPR_PREDICT_MEAN || !fmode) {
     // nothing to fuse for the mean alone (mu = K(xp, x) alpha); or the unfused reference order
     double* wt = dalpha;
     if (!wt) {
@@ -312,7 +317,7 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, W, n));
   HIP_TRY(ctx, hipMemcpy2DAsync(Z, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
                                 (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
-  RhsSpec rhs{W, m + nrhs, n, 0};
+  RhsSpec rhs{W, m + nrhs, n, 0, fmode == 2 ? 2 : 1};
   int hinfo = 0;
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
   if (info) *info = hinfo;
@@ -451,6 +456,9 @@ static int run_children(gpr_ctx* ctx, int nsub, const std::function<int(gpr_ctx*
       hipFree(c->dbig);
       c->dbig = nullptr;
       c->big_cap = 0;
+      if (c->dbig2) hipFree(c->dbig2);  // fused fit+predict workspace of the folds
+      c->dbig2 = nullptr;
+      c->big2_cap = 0;
       c->fac_valid = false;  // cached factor data were keyed on pointers into dbig
       c->sqinv_nb2 = 0;
     }

@@ -127,6 +127,30 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (mode == 5) {
+    // the factorisation's trailing SYRK in place: C = A(r:, r:) -= A(k:k+K, r:)^T A(k:k+K, r:)
+    // inside an N x N matrix (ld N), trailing width W (argv[4]), vs mode 0's dense operands
+    const int W = argc > 4 ? atoi(argv[4]) : N / 2;
+    double* A5;
+    hipMalloc(&A5, sizeof(double) * (size_t)N * N);
+    init_kernel<<<1024, 256, 0, s>>>(A5, (size_t)N * N, 5);
+    const int r = N - W, k = r - K;
+    GemmArgs g{};
+    g.P = A5 + k + (size_t)r * N; g.ldp = N;
+    g.Q = g.P; g.ldq = N;
+    g.C = A5 + r + (size_t)r * N; g.ldc = N;
+    g.M = W; g.N = W; g.K = K; g.alpha = -1.0; g.beta = 1.0; g.upper = 1;
+    const double flops = (double)W * (W + 1) * K;
+    for (int rep = 0; rep < 5; ++rep) {
+      hipEventRecord(e0, s);
+      launch_gemm_tn(ctx, g, TC_OTHER);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+      float ms; hipEventElapsedTime(&ms, e0, e1);
+      if (rep >= 2) printf("in-place syrk N=%d W=%d K=%d: %.3f ms  %.2f TFLOP/s\n", N, W, K, ms, flops / ms / 1e9);
+    }
+    return 0;
+  }
   if (mode == 3) {
     // general C (M x N, ldc) -= P^T Q with P K x M (ldp), Q K x N (ld K): TRSM-update shapes
     const int M = argc > 4 ? atoi(argv[4]) : N;

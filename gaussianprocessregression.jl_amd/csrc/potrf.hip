@@ -1760,6 +1760,45 @@ int rhs_panel_step(gpr_ctx* ctx, const double* dU, int n, int ldu, const RhsSpec
 
 }  // namespace
 
+// Debug timing of the chain kernels (tools/gemm_bench mode 6 only), averaged over the
+// diagonal blocks 0 .. reps-1 of a freshly assembled SPD matrix A (each factored once):
+// variant 0 the diagonal-block kernel (U + W), 1 the W^T GEMM row TRSM (after variant 0).
+extern "C" int gpr_debug_chain_kernels(gpr_ctx_t ctx, double* A, int lda, int n, int variant,
+                                       int reps, float* ms) {
+  GPR_TRY(ensure_winv(ctx, n, 128));
+  reps = std::min(reps, n / 128 - 1);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  ctx->ls = ctx->stream;
+  HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
+  hipEventRecord(e0, ctx->stream);
+  for (int r = 0; r < reps; ++r) {
+    const int j = 128 * r;
+    double* wj = ctx->winv + (size_t)r * 128 * 128;
+    if (variant == 0) GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
+    if (variant == 1) {
+      GemmArgs g{};
+      g.P = wj; g.ldp = 128;
+      g.Q = A + j + (size_t)(j + 128) * lda; g.ldq = lda;
+      g.C = A + j + (size_t)(j + 128) * lda; g.ldc = lda;
+      g.M = 128; g.N = n - j - 128; g.K = 128;
+      g.alpha = 1.0; g.beta = 0.0;
+      g.info = ctx->dinfo;
+      GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
+    }
+  }
+  hipEventRecord(e1, ctx->stream);
+  hipEventSynchronize(e1);
+  hipEventElapsedTime(ms, e0, e1);
+  *ms /= reps;
+  int hinfo = 0;
+  hipMemcpy(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return hinfo;
+}
+
 // Two-level right-looking upper Cholesky with depth-1 lookahead.
 //   outer panels P_s = rows [s*nb2, (s+1)*nb2)      (nb2 = K of the big MFMA updates)
 //   stream2 (panel):  wait b_{s-1}; a_s = update of rows P_{s+1} by P_s; factor P_{s+1}

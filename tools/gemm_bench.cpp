@@ -45,6 +45,8 @@ __global__ void verify_kernel(const double* P, const double* C, int N, int K, in
 }
 
 extern "C" void gpr_debug_diag_stamps(unsigned long long* out);
+extern "C" int gpr_debug_chain_kernels(gpr_ctx_t ctx, double* A, int lda, int n, int variant,
+                                       int reps, float* ms);
 
 int main(int argc, char** argv) {
   int N = argc > 1 ? atoi(argv[1]) : 16384;
@@ -124,6 +126,25 @@ int main(int argc, char** argv) {
         gpr_timing_get(ctx, c, &tms, &ln, &fl);
         if (ln) printf("  %-9s %8.2f ms %5lld launches %7.2f TF\n", nm[c], tms, ln, fl / tms / 1e9);
       }
+    }
+    return 0;
+  }
+  if (mode == 6) {
+    // chain kernels on the diagonal blocks of an SE+WN matrix (gpr_debug_chain_kernels)
+    int d = 8;
+    double *X, *A;
+    hipMalloc(&X, sizeof(double) * d * N);
+    hipMalloc(&A, sizeof(double) * (size_t)N * N);
+    init_kernel<<<1024, 256, 0, s>>>(X, (size_t)d * N, 7);
+    int kinds[2] = {GPR_SE, GPR_WN};
+    std::vector<double> hp(d + 2, 3.0);
+    hp[0] = 1.0; hp[d + 1] = 0.1;
+    const char* nm[2] = {"diag (U + W)", "row TRSM W^T GEMM"};
+    gpr_kernel(ctx, kinds, 2, hp.data(), d, X, N, nullptr, N, 1, 1e-8, A, N);
+    for (int v = 0; v < 2; ++v) {
+      float ms = 0;
+      const int info = gpr_debug_chain_kernels(ctx, A, N, N, v, 60, &ms);
+      printf("N=%d %-24s %8.2f us per launch (info %d)\n", N, nm[v], ms * 1e3, info);
     }
     return 0;
   }

@@ -77,6 +77,34 @@ __global__ void storepair_kernel(double* K, int N, int ntiles) {
   }
 }
 
+// the symmetric write shape with TH x TH tiles walked in S x S super-tiles (super-tiles in
+// column-triangular order, tiles inside column-major; below-diagonal tiles of diagonal
+// super-tiles idle): the active workgroups write S*TH-row runs in both orientations
+template <int TH, int S>
+__global__ void storepair_super_kernel(double* K, int N, int nslots) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  constexpr int LPC = TH / 2, CPI = 256 / LPC;  // lanes per column, columns per instruction
+  const int lr = threadIdx.x % LPC, cg = threadIdx.x / LPC;
+  for (int b = blockIdx.x; b < nslots; b += gridDim.x) {
+    const int sidx = b / (S * S), loc = b % (S * S);
+    int sj = (int)((sqrt(8.0 * sidx + 1.0) - 1.0) * 0.5);
+    while ((sj + 1) * (sj + 2) / 2 <= sidx) ++sj;
+    while (sj * (sj + 1) / 2 > sidx) --sj;
+    const int si = sidx - sj * (sj + 1) / 2;
+    const int bi = si * S + loc % S, bj = sj * S + loc / S;
+    if (bi > bj) continue;
+    double* base = K + (size_t)bi * TH + 2 * lr + ((size_t)bj * TH + cg) * N;
+#pragma unroll
+    for (int c = 0; c < TH / CPI; ++c)
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)CPI * c * N));
+    if (bi == bj) continue;
+    double* mb = K + (size_t)bj * TH + 2 * lr + ((size_t)bi * TH + cg) * N;
+#pragma unroll
+    for (int c = 0; c < TH / CPI; ++c)
+      __builtin_nontemporal_store(d2{3.0, 4.0}, reinterpret_cast<d2*>(mb + (size_t)CPI * c * N));
+  }
+}
+
 // one 16-B store per thread, no loop (the blit-kernel shape)
 __global__ void store16flat_kernel(double* p) {
   typedef double d2 __attribute__((ext_vector_type(2)));
@@ -186,6 +214,29 @@ int main(int argc, char** argv) {
       timeit([&] { store16x4_kernel<<<g, 256, 0, s>>>(K, bytes / 16); }, nm);
     }
     timeit([&] { store16flat_kernel<<<(unsigned)(bytes / 16 / 256), 256, 0, s>>>(K); }, "store16flat");
+    {
+      auto slots = [&](int th, int S) {
+        const int ns = N / th / S;
+        return ns * (ns + 1) / 2 * S * S;
+      };
+      for (int g : {1024, 2048, 4096}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "pair64 S1 grid %d", g);
+        timeit([&] { storepair_super_kernel<64, 1><<<g, 256, 0, s>>>(K, N, slots(64, 1)); }, nm);
+        snprintf(nm, sizeof nm, "pair64 S8 grid %d", g);
+        timeit([&] { storepair_super_kernel<64, 8><<<g, 256, 0, s>>>(K, N, slots(64, 8)); }, nm);
+        snprintf(nm, sizeof nm, "pair64 S16 grid %d", g);
+        timeit([&] { storepair_super_kernel<64, 16><<<g, 256, 0, s>>>(K, N, slots(64, 16)); }, nm);
+        snprintf(nm, sizeof nm, "pair128 S1 grid %d", g);
+        timeit([&] { storepair_super_kernel<128, 1><<<g, 256, 0, s>>>(K, N, slots(128, 1)); }, nm);
+        snprintf(nm, sizeof nm, "pair128 S4 grid %d", g);
+        timeit([&] { storepair_super_kernel<128, 4><<<g, 256, 0, s>>>(K, N, slots(128, 4)); }, nm);
+        snprintf(nm, sizeof nm, "pair128 S8 grid %d", g);
+        timeit([&] { storepair_super_kernel<128, 8><<<g, 256, 0, s>>>(K, N, slots(128, 8)); }, nm);
+        snprintf(nm, sizeof nm, "pair256 S4 grid %d", g);
+        timeit([&] { storepair_super_kernel<256, 4><<<g, 256, 0, s>>>(K, N, slots(256, 4)); }, nm);
+      }
+    }
     {
       const int ntl = (N / 64) * (N / 64), ntp = (N / 64) * (N / 64 + 1) / 2;
       timeit([&] { storetile_kernel<<<ntl, 256, 0, s>>>(K, N, ntl); }, "storetile 1 tile/WG");

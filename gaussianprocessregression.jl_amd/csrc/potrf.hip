@@ -1272,11 +1272,14 @@ static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int 
 static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
 
 static int factor_panel_inv(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
+static int factor_panel_rec(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
 
 int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
   if (ctx->panel_mode == 3 && ctx->nb == 128 && ctx->diag_cus == 0 && !ctx->inner_la &&
       n - k - kw >= std::max(1, ctx->inv_strip_min) && ctx->nb2 <= 2048 && ctx->nb2 >= 128)
     return factor_panel_inv(ctx, A, n, lda, k, kw);
+  if (ctx->panel_mode == 4 && ctx->diag_cus == 0 && !ctx->inner_la)
+    return factor_panel_rec(ctx, A, n, lda, k, kw);
   if (ctx->panel_mode == 2 && ctx->stream3 && ctx->diag_cus == 0 && !ctx->inner_la)
     return factor_panel_ll(ctx, A, n, lda, k, kw);
   if (ctx->inner_la == 2 && ctx->stream3 && ctx->diag_cus == 0)
@@ -1509,6 +1512,45 @@ static int factor_panel_inv(gpr_ctx* ctx, double* A, int n, int lda, int k, int 
                                 sizeof(double) * kw, sizeof(double) * kw, nrest,
                                 hipMemcpyDeviceToDevice, ctx->ls));
   return 0;
+}
+
+// Recursive panel (GPR_PANEL=4): rows [k, k+kw) factored by halves -- the left half of the
+// panel rows recursively (its row TRSMs full width), then ONE update of the right half's rows
+// over all columns right of them with K = kw/2, then the right half.  Same flops and the same
+// chain of diagonal blocks as the per-block loop, but the in-panel updates run at K = 512,
+// 256, 128 (half, a quarter, a quarter of the work) instead of all at K = 128, so the panel
+// stream takes less CU time from the trailing SYRK it overlaps.
+static int factor_panel_rec(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
+  const int nb = ctx->nb;
+  if (kw <= nb) {
+    const int jb = std::min(nb, n - k);
+    double* wj = ctx->winv + (size_t)(k / nb) * nb * nb;
+    GPR_TRY(launch_diag(ctx, A, lda, n, k, wj, 1, 1));
+    if (k + jb >= n) return 0;
+    double* row = A + k + (size_t)(k + jb) * lda;
+    GemmArgs g{};
+    g.P = wj; g.ldp = nb;
+    g.Q = row; g.ldq = lda;
+    g.C = row; g.ldc = lda;
+    g.M = jb; g.N = n - k - jb; g.K = jb;
+    g.alpha = 1.0; g.beta = 0.0;
+    g.info = ctx->dinfo;
+    return launch_gemm_tn(ctx, g, TC_PANEL);
+  }
+  const int h = ((kw / nb + 1) / 2) * nb;  // left half, whole blocks
+  GPR_TRY(factor_panel_rec(ctx, A, n, lda, k, h));
+  const int r0 = k + h, rows = kw - h;
+  if (rows <= 0 || r0 >= n) return 0;
+  GemmArgs u{};
+  u.P = A + k + (size_t)r0 * lda; u.ldp = lda;   // U(k:k+h, r0:r0+rows)
+  u.Q = u.P; u.ldq = lda;                         // U(k:k+h, r0:n)
+  u.C = A + r0 + (size_t)r0 * lda; u.ldc = lda;
+  u.M = rows; u.N = n - r0; u.K = h;
+  u.alpha = -1.0; u.beta = 1.0;
+  u.mask_upper = 1;
+  u.info = ctx->dinfo;
+  GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
+  return factor_panel_rec(ctx, A, n, lda, r0, rows);
 }
 
 // Block lookahead (GPR_INNER_LA=2): the chain stream carries only what the next diagonal

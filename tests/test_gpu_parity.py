@@ -200,14 +200,14 @@ def test_potrf_upper(n, nb):
 def _panel_env(monkeypatch, mode):
     """Panel schedule under test: "0" per-block full-width panel, "1" square-panel kernel,
     "la2" block lookahead, "ll" square chain + left-looking strip (GPR_PANEL=2), "inv" square
-    chain + strip by the square's inverse (GPR_PANEL=3)."""
+    chain + strip by the square's inverse (GPR_PANEL=3), "rec" recursive halves (GPR_PANEL=4)."""
     monkeypatch.setenv("GPR_PANEL_SQ", mode if mode in ("0", "1") else "0")
     monkeypatch.setenv("GPR_INNER_LA", "2" if mode == "la2" else "0")
-    monkeypatch.setenv("GPR_PANEL", {"ll": "2", "inv": "3"}.get(mode, "0"))
+    monkeypatch.setenv("GPR_PANEL", {"ll": "2", "inv": "3", "rec": "4"}.get(mode, "0"))
     monkeypatch.setenv("GPR_INV_STRIP_MIN", "1")  # "inv": every panel with a strip
 
 
-@pytest.mark.parametrize("panel_sq", ["1", "0", "la2", "ll", "inv"])
+@pytest.mark.parametrize("panel_sq", ["1", "0", "la2", "ll", "inv", "rec"])
 @pytest.mark.parametrize("n,nb2", [(300, 256), (1000, 256), (1300, 512), (2600, 1024), (1024, 1024),
                                    (1025, 1024), (777, 2048), (3000, 384)])
 def test_potrf_outer_panels(n, nb2, panel_sq, monkeypatch):
@@ -231,7 +231,7 @@ def test_potrf_outer_panels(n, nb2, panel_sq, monkeypatch):
     assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
 
 
-@pytest.mark.parametrize("panel_sq", ["1", "0", "la2", "ll", "inv"])
+@pytest.mark.parametrize("panel_sq", ["1", "0", "la2", "ll", "inv", "rec"])
 @pytest.mark.parametrize("j", [0, 255, 256, 700, 1299])
 def test_potrf_not_posdef_info_later_panels(j, panel_sq, monkeypatch):
     _panel_env(monkeypatch, panel_sq)

@@ -64,7 +64,8 @@ struct gpr_ctx {
                                   // fused_rhs_nmax), 0 off, 1/2 forced (GPR_FUSED_RHS)
   int fused_rhs_nmax = 16384;     // GPR_FUSED_RHS_NMAX
   int fuse_y = 0;
-  int fuse_kinv = 1;              // gpr_fit_kinv: Z = U^{-T} solved inside the factorisation                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
+  int fuse_kinv = 2;              // gpr_fit_kinv: Z = U^{-T} solved inside the factorisation
+                                  // (1), and K^{-1} = Z^T Z accumulated there too (2)                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   std::vector<hipEvent_t> sync_events;
@@ -200,6 +201,10 @@ struct RhsSpec {
   int ldb;
   int lower_rhs;
   int mode;  // 1: own stream (srhs) beside the trailing updates; 2: main stream after each SYRK
+  // optional: gram (ldg) += X_s^T X_s (upper, columns < the panel end) after each solved
+  // panel X_s of B -- K^{-1} = Z^T Z accumulated panel by panel when B is the identity
+  double* gram;
+  int ldg;
 };
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
                const RhsSpec* rhs = nullptr);

@@ -1904,7 +1904,19 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     if (!sr) return 0;
     ctx->ls = sr;
     HIP_TRY(ctx, hipStreamWaitEvent(sr, ev_sq, 0));
-    return rhs_panel_step(ctx, dA, n, lda, *rhs, k, nb2, ctx->dpanel_rhs);
+    GPR_TRY(rhs_panel_step(ctx, dA, n, lda, *rhs, k, nb2, ctx->dpanel_rhs));
+    if (!rhs->gram) return 0;
+    // rows [k, kend) of the solved B are final: gram(0:kend, 0:kend) += B_s^T B_s (upper)
+    const int kend = std::min(n, k + nb2);
+    GemmArgs g{};
+    g.P = rhs->B + k; g.ldp = rhs->ldb;
+    g.Q = rhs->B + k; g.ldq = rhs->ldb;
+    g.C = rhs->gram; g.ldc = rhs->ldg;
+    g.M = kend; g.N = kend; g.K = kend - k;
+    g.alpha = 1.0; g.beta = 1.0;
+    g.upper = 1;
+    g.info = ctx->dinfo;
+    return launch_gemm_tn(ctx, g, TC_TRSM_GEMM);
   };
   int rc = panel(0, std::min(nb2, n));
   hipEvent_t ev_p = sync_event(ctx, ev++);

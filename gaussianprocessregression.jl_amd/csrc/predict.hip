@@ -196,7 +196,7 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, co
   int hinfo = 0;
   if (ctx->fuse_y) {
     // z = U^{-T} y solved inside the factorisation (side stream), then the backward sweep
-    RhsSpec rhs{dalpha, nrhs, n, 0, ctx->fused_rhs == 2 ? 2 : 1};
+    RhsSpec rhs{dalpha, nrhs, n, 0, ctx->fused_rhs == 2 ? 2 : 1, nullptr, 0};
     GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
     if (info) *info = hinfo;
     if (hinfo != 0) return hinfo;
@@ -266,12 +266,22 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   int hinfo = 0;
   // Z = U^{-T} (identity right-hand side, lower triangular) solved in the factorisation's
   // lookahead bubbles (GPR_FUSE_KINV=0: after it, as gpr_potri_upper)
-  RhsSpec rhs{Z, n, n, 1, ctx->fused_rhs == 2 ? 2 : 1};
+  // GPR_FUSE_KINV=2 (default) also accumulates K^{-1} += Z_s^T Z_s as each row panel Z_s is
+  // solved, so the N^3/3-flop Gram product fills the chain-bound half of the factorisation
+  // instead of running after it
+  RhsSpec rhs{Z, n, n, 1, ctx->fused_rhs == 2 ? 2 : 1, nullptr, 0};
+  if (ctx->fuse_kinv == 2) {
+    HIP_TRY(ctx, hipMemset2DAsync(dKinv, (size_t)ldkinv * sizeof(double), 0,
+                                  (size_t)n * sizeof(double), n, ctx->stream));
+    rhs.gram = dKinv;
+    rhs.ldg = ldkinv;
+  }
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, ctx->fuse_kinv ? &rhs : nullptr));
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
   GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
   if (!ctx->fuse_kinv) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
+  if (rhs.gram) return launch_mirror_upper(ctx, dKinv, n, ldkinv);
   return kinv_from_z(ctx, Z, n, dKinv, ldkinv);
 }
 
@@ -317,7 +327,7 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, W, n));
   HIP_TRY(ctx, hipMemcpy2DAsync(Z, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
                                 (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
-  RhsSpec rhs{W, m + nrhs, n, 0, fmode == 2 ? 2 : 1};
+  RhsSpec rhs{W, m + nrhs, n, 0, fmode == 2 ? 2 : 1, nullptr, 0};
   int hinfo = 0;
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
   if (info) *info = hinfo;

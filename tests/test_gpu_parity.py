@@ -689,11 +689,12 @@ def test_fit_predict_multi_output_and_reuse():
     assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("fuse", ["2", "1", "0"])
 @pytest.mark.parametrize("n,nb2", [(300, None), (1300, 256), (2100, 1024), (777, 512)])
 def test_fit_kinv(n, nb2, fuse, monkeypatch):
     """gpr_fit_kinv = update_cache!(::MllGradCache) (src/cost.jl:83-111): U, alpha and the
-    dense K^{-1}, with Z = U^{-T} solved inside the factorisation (fuse=1) or after it."""
+    dense K^{-1}, with Z = U^{-T} solved inside the factorisation and K^{-1} = Z^T Z
+    accumulated there panel by panel (fuse=2), Z alone inside (fuse=1), or both after it."""
     monkeypatch.setenv("GPR_FUSE_KINV", fuse)
     kinds = KSETS["SE+WN"]
     dim = 4

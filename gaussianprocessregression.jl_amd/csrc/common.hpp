@@ -31,7 +31,8 @@ struct KParams {
 // TC_GEMM_PIPE is kernel-level (every launch of the pipelined 2-WG/CU GEMM, whatever its call
 // site), recorded in addition to the call-site class.
 enum TimingClass {
-  TC_KBUILD = 0, TC_SYRK = 1, TC_PANEL = 2, TC_TRSM_GEMM = 3, TC_OTHER = 4, TC_GEMM_PIPE = 5, TC_N = 6
+  TC_KBUILD = 0, TC_SYRK = 1, TC_PANEL = 2, TC_TRSM_GEMM = 3, TC_OTHER = 4, TC_GEMM_PIPE = 5,
+  TC_DAG = 6, TC_N = 7
 };
 
 struct TimedLaunch {
@@ -68,6 +69,15 @@ struct gpr_ctx {
                                   // (1), and K^{-1} = Z^T Z accumulated there too (2)                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
+  // persistent tile-DAG factorisation (dag.hip): 0 off, 1 on for dag_nmin <= n <= dag_nmax
+  // (GPR_DAG, GPR_DAG_NMIN, GPR_DAG_NMAX); the task list is cached per (tiles, rhs tiles)
+  int dag_mode = 0;
+  int dag_nmin = 0, dag_nmax = 1 << 30;
+  unsigned* dag_tasks = nullptr;
+  int dag_ntasks = 0, dag_nt = -1, dag_ntr = -1;
+  int* dag_sync = nullptr;
+  size_t dag_sync_cap = 0;
+  int ncu = 0;
   std::vector<hipEvent_t> sync_events;
   size_t ev_next = 0;
 
@@ -206,6 +216,8 @@ struct RhsSpec {
   double* gram;
   int ldg;
 };
+// one-launch tile-DAG factorisation (+ B <- U^{-T} B); 1 = shape not eligible, 0 = launched
+int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb);
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
                const RhsSpec* rhs = nullptr);
 int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);

@@ -1,0 +1,441 @@
+// Persistent tile-DAG Cholesky (dpotrf 'U', in place) with optional fused right-hand sides
+// B <- U^{-T} B, in ONE launch.
+//
+// Replaces the same reference calls as potrf_core (cholesky!(Hermitian(K)), src/cost.jl:77,
+// src/predict.jl:31) and, with B, the first half of ldiv!/rdiv! against the factor
+// (src/predict.jl:32,84: V = U^{-T} K(x, xp) and z = U^{-T} y in gpr_fit_predict).
+//
+// Left-looking by 128 x 128 tile: the task of upper tile (i, j) of A owns that tile for its
+// whole life:
+//     acc  = A_ij - sum_{k<i} U_ki^T U_kj          (one long-K FP64 MFMA accumulation)
+//     i == j:  U_ii = chol(acc), W_i = U_ii^{-1}   (diag_block.hpp, in LDS)
+//     i <  j:  U_ij = W_i^T acc                     (one K = 128 product)
+// and the task of right-hand-side tile (i, c) the same with B's column block c in place of
+// A's column block j.  A tile is written by its task only, and read by other tasks only
+// after it is final, so no XCD's L2 or CU's L1 can hold a stale copy of data another
+// workgroup reads: final tiles (and W_i) are stored with sc1 (write-through; the line leaves
+// the writer's L2), then a per-column progress counter is raised with an sc1 store after
+// the stores drained (the MI355X guide's sc1 hand-off: no L2 write-back, no L1 invalidate).
+// colprog[j] = number of final tiles at the top of column block j of A (tiles (0..p-1, j));
+// rhsprog[c] likewise for B.  Column tiles finalise top-down, so one counter per column
+// suffices; a task accumulates row blocks as their tiles become final (k < min(colprog[i],
+// colprog[j])), so only its last row block waits for the previous row.
+//
+// Scheduling: one workgroup per CU (128 KB of LDS: four 32-KB DMA stages of the GEMM
+// pipeline, or the diagonal block), tasks claimed from an atomic ticket in a host-built
+// topological order (row i of A's tiles, then row i of B's tiles, for i = 0, 1, ...): every
+// tile a task waits for belongs to an earlier ticket, i.e. to a workgroup that is already
+// running, so the grid cannot deadlock whatever the residency.  Every wait is bounded
+// (~seconds): on timeout the launch flags info = -1 and every task still publishes, so the
+// grid always drains.  A non-positive pivot sets info (first failure wins; later pivots
+// depend on it) and the remaining tasks skip their arithmetic.
+//
+// Conditions (checked by the host): tiles of 128, n % 16 == 0, lda % 16 == 0 (and ldb),
+// 128-B aligned bases -- every 128-B line then belongs to exactly one tile.
+#include <algorithm>
+#include <cstdint>
+
+#include "diag_block.hpp"
+
+#ifdef DAG_TRACE
+// diagnostic build only (tools/probe/dag_probe): per-workgroup progress words
+__device__ int g_dag_trace[4096];
+#define DTRACE(slot, v)                                                                   \
+  do {                                                                                    \
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)                            \
+      __hip_atomic_store(&g_dag_trace[blockIdx.x * 8 + (slot)], (v), __ATOMIC_RELAXED,     \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                      \
+  } while (0)
+extern "C" void gpr_debug_dag_trace(int* out, void* stream) {
+  hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_dag_trace), sizeof(int) * 4096, 0,
+                           hipMemcpyDeviceToHost, (hipStream_t)stream);
+  hipStreamSynchronize((hipStream_t)stream);
+}
+#else
+#define DTRACE(slot, v) \
+  do {                  \
+  } while (0)
+#endif
+
+namespace {
+
+constexpr int DT = 128;                     // tile edge
+constexpr int DTK = 16;                     // K rows per pipeline stage
+constexpr int DPB = 4;                      // LDS stages
+constexpr int DSTAGE = (DT + DT) * DTK;     // doubles per stage (P image, then Q)
+constexpr int DLDS = DPB * DSTAGE;          // 16384 doubles = 128 KB
+constexpr int DNCH = DTK / 2;               // 16-B chunks per LDS row
+constexpr int DRPD = 64 / DNCH;             // rows per wave-wide 1-KB DMA
+constexpr int DNDMA = DT / (4 * DRPD);      // DMA instructions per wave per operand
+constexpr int DVM = 2 * DNDMA;              // vmcnt increments per stage
+constexpr int DNP = DTK / 8;                // fragment blocks (2 k-steps each) per stage
+static_assert(D2_PK + 4 * D2_PB + 2 <= DLDS, "diagonal block must fit in the stage buffers");
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+struct DagArgs {
+  double* A;
+  size_t lda;
+  int n, nt;
+  double* B;  // optional right-hand sides (n x nrhs, ld ldb)
+  size_t ldb;
+  int nrhs, ntr;
+  double* winv;  // W_i = U_ii^{-1} in slot i (128 x 128)
+  int kglob;     // global index of row 0 (reported pivot orders)
+  int* info;
+  int* sync;     // [0] ticket, [2 + j] colprog[j], [2 + nt + c] rhsprog[c]
+  const unsigned* tasks;
+  int ntasks;
+};
+
+__device__ __forceinline__ int ld_sc1(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int VM>
+__device__ __forceinline__ void dag_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
+}
+
+__device__ __forceinline__ int dag_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int dag_idx(int row, int chunk) {
+  return row * DTK + ((chunk ^ dag_swz(row)) << 1);
+}
+
+// acc[i][j][r] += sum_{k < 16 nst} P[k + m ldp] Q[k + n ldq] for the tile element
+// (m, n) = (64 wm + 16 j + (lane & 15), 64 wn + 16 i + (lane >> 4) + 4 r)  (gemm.hip's layout:
+// the Q fragment is the MFMA A operand).  Rows m >= mv / n >= nv are clamped (their results
+// are never stored).  The pipelined gemm.hip body at one workgroup per CU: four LDS stages
+// fed by LDS-DMA (global_load_lds_dwordx4, swizzle applied on the source address), DMA three
+// stages ahead, next stage's fragments read during the current stage's MFMAs.  Leaves the
+// LDS free (ends with a barrier).
+__device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __restrict__ P,
+                                          size_t ldp, int mv, const double* __restrict__ Q,
+                                          size_t ldq, int nv, int nst, double* lds) {
+  if (nst <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  const double* srcP[DNDMA];
+  const double* srcQ[DNDMA];
+#pragma unroll
+  for (int r = 0; r < DNDMA; ++r) {
+    const int row = DRPD * (4 * r + w) + lane / DNCH;
+    const int c = (lane % DNCH) ^ dag_swz(row);
+    srcP[r] = P + 2 * c + (size_t)min(row, mv - 1) * ldp;
+    srcQ[r] = Q + 2 * c + (size_t)min(row, nv - 1) * ldq;
+  }
+  auto issue = [&](int s) {
+    double* base = lds + (s % DPB) * DSTAGE;
+    const size_t ko = (size_t)min(s, nst - 1) * DTK;
+#pragma unroll
+    for (int r = 0; r < DNDMA; ++r) {
+      __builtin_amdgcn_global_load_lds(srcP[r] + ko, base + (4 * r + w) * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(srcQ[r] + ko, base + DT * DTK + (4 * r + w) * 128, 16, 0, 0);
+    }
+  };
+  auto read_frags = [&](d2 (&F)[DNP][8], int s) {
+    const double* ps = lds + (s % DPB) * DSTAGE;
+    const double* qs = ps + DT * DTK;
+#pragma unroll
+    for (int p = 0; p < DNP; ++p) {
+      const int ch = (lane >> 4) + 4 * p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        F[p][i] = *reinterpret_cast<const d2*>(&qs[dag_idx(wn * 64 + i * 16 + (lane & 15), ch)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        F[p][4 + j] = *reinterpret_cast<const d2*>(&ps[dag_idx(wm * 64 + j * 16 + (lane & 15), ch)]);
+    }
+  };
+  auto mfma_stage = [&](const d2 (&F)[DNP][8]) {
+#pragma unroll
+    for (int p = 0; p < DNP; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[p][i][h], F[p][4 + j][h], acc[i][j], 0, 0, 0);
+  };
+  auto step = [&](int s, d2 (&Fc)[DNP][8], d2 (&Fn)[DNP][8]) {
+    dag_vmcnt<DVM>();  // own DMA of stage s+1 retired, stage s+2 still in flight
+    __builtin_amdgcn_s_barrier();
+    issue(s + 3);
+    read_frags(Fn, s + 1);
+    mfma_stage(Fc);
+#pragma unroll
+    for (int t = 0; t < DVM; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    }
+#pragma unroll
+    for (int t = 0; t < 8 * DNP; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - DVM - 16 * DNP, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+  };
+  d2 F0[DNP][8], F1[DNP][8];
+  issue(0);
+  issue(1);
+  issue(2);
+  dag_vmcnt<2 * DVM>();
+  __builtin_amdgcn_s_barrier();
+  read_frags(F0, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  int s = 0;
+  for (; s + 1 < nst; s += 2) {
+    step(s, F0, F1);
+    step(s + 1, F1, F0);
+  }
+  if (s < nst) mfma_stage(F0);
+  dag_vmcnt<0>();
+  __syncthreads();
+}
+
+// Control flow around barriers must be WAVE-UNIFORM: a thread-0-only region (exec-masked)
+// next to the barriers of the task loop was structurised by the compiler so that the publish
+// store ran under a mask no lane satisfied and the grid hung.  So every "one lane" action
+// below is done by all 64 lanes of wave 0 behind a scalar branch on the wave index (same
+// value to the same address), and values steering branches are readfirstlane'd.
+
+// Block until min(pa, pb) > have (wave 0 polls with sc1 loads, sleeping between polls);
+// returns min(pa, pb, cap), uniform across the workgroup.  Bounded: after ~2^25 polls the
+// launch is flagged (info = -1) and the wait returns cap (results are garbage, the grid drains).
+__device__ __forceinline__ int dag_wait(const int* pa, const int* pb, int have, int cap,
+                                        int* info, int* sh) {
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+    int v = 0;
+    long long spins = 0;
+    for (;;) {
+      v = __builtin_amdgcn_readfirstlane(min(ld_sc1(pa), ld_sc1(pb)));
+      if (v > have) break;
+      if (++spins > (1ll << 25)) {
+        atomicCAS(info, 0, -1);
+        v = cap;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *sh = min(v, cap);
+  }
+  // no instruction: keeps the compiler from hoisting the data loads above the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  __syncthreads();
+  const int r = __builtin_amdgcn_readfirstlane(*sh);
+  __syncthreads();  // *sh may be rewritten by the next wait
+  return r;
+}
+
+// stores of the drained task become visible before the counter: every storing wave waits
+// for its stores, then wave 0 raises the counter (sc1)
+__device__ __forceinline__ void dag_publish(int* prog, int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
+    __hip_atomic_store(prog, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The F task's factorisation, out of line: inlined, its readlane-heavy elimination (SGPR
+// spills into VGPR lanes) shares the allocation with the GEMM pipeline's live state and
+// spilled to scratch; as a call it is allocated on its own.
+__device__ __attribute__((noinline)) int dag_factor(double* S, double* T, size_t lda, int mv,
+                                                     int kglob, double* winv) {
+  double(*Xd)[D2_PB] = reinterpret_cast<double(*)[D2_PB]>(S + D2_PK);
+  int* fail = reinterpret_cast<int*>(S + D2_PK + 4 * D2_PB);
+  return diag2_core<true>(S, Xd, fail, T, lda, mv, kglob, winv);
+}
+
+__global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
+  __shared__ double lds[DLDS];
+  __shared__ int s_task, s_skip, s_wait;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  int* colprog = a.sync + 2;
+  int* rhsprog = colprog + a.nt;
+  for (;;) {
+    if (w == 0) {  // one ticket: lane 0 adds 1, the other lanes 0 (a wave-wide atomic)
+      const int tk = atomicAdd(&a.sync[0], lane == 0 ? 1 : 0);
+      const int tk0 = __builtin_amdgcn_readlane(tk, 0);
+      s_task = tk0;
+      s_skip = __builtin_amdgcn_readfirstlane(ld_sc1(a.info)) != 0;
+    }
+    __syncthreads();
+    // wave-uniform (SGPR) copies: the loop exit and every branch around the barriers below
+    // must be provably uniform, or the compiler structurises them as divergent and the
+    // thread-0 publish ends up under a mask no lane satisfies (observed: the grid hangs)
+    const int t = __builtin_amdgcn_readfirstlane(s_task);
+    const bool skip = __builtin_amdgcn_readfirstlane(s_skip);
+    DTRACE(0, t);
+    DTRACE(1, 1);
+    if (t >= a.ntasks) break;
+    const unsigned code = __builtin_amdgcn_readfirstlane(a.tasks[t]);  // (a vector load)
+    const bool rhs = code >> 31;
+    const int i = (code >> 16) & 0x7fff, j = code & 0xffff;
+    const bool diag = !rhs && i == j;
+    double* T = rhs ? a.B + (size_t)i * DT + (size_t)j * DT * a.ldb
+                    : a.A + (size_t)i * DT + (size_t)j * DT * a.lda;
+    const size_t ldt = rhs ? a.ldb : a.lda;
+    const double* Qcol = rhs ? a.B + (size_t)j * DT * a.ldb : a.A + (size_t)j * DT * a.lda;
+    const double* Pcol = a.A + (size_t)i * DT * a.lda;
+    int* pj = rhs ? rhsprog + j : colprog + j;
+    const int mv = min(DT, a.n - i * DT);                        // rows of the tile
+    const int nv = min(DT, (rhs ? a.nrhs : a.n) - j * DT);       // columns of the tile
+    if (!skip) {
+      // acc = -T (the result is -acc after the accumulation), branch-free clamped loads
+      d4v acc[4][4];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+          const double* col = T + (size_t)min(nn, nv - 1) * ldt;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int mm = wm * 64 + jj * 16 + (lane & 15);
+            const double c = col[min(mm, mv - 1)];
+            acc[ii][jj][r] = (mm < mv && nn < nv) ? -c : 0.0;
+          }
+        }
+      // acc += sum_{k<i} U_ki^T X_kj, row blocks taken as soon as both columns have them final
+      DTRACE(1, 2);
+      int done = 0;
+      while (done < i) {
+        const int r = dag_wait(colprog + i, pj, done, i, a.info, &s_wait);
+        dag_accum(acc, Pcol + (size_t)done * DT, a.lda, mv, Qcol + (size_t)done * DT, ldt, nv,
+                  (r - done) * (DT / DTK), lds);
+        done = r;
+      }
+      if (diag) {
+        // factor -acc in LDS (packed upper, identity padding beyond mv), U_ii and W_i out (sc1)
+        double* S = lds;
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int mm = wm * 64 + jj * 16 + (lane & 15);
+              if (mm <= nn) S[pk(mm, nn)] = nn < mv ? -acc[ii][jj][r] : (mm == nn ? 1.0 : 0.0);
+            }
+          }
+        __syncthreads();
+        DTRACE(1, 3);
+        const int f = dag_factor(S, T, a.lda, mv, a.kglob + i * DT, a.winv + (size_t)i * DT * DT);
+        if (f && w == 0) atomicCAS(a.info, 0, f);
+        DTRACE(1, 4);
+      } else {
+        // B_ij = -acc into the tile (own tile: only this workgroup reads it back), then
+        // U_ij = W_i^T B_ij once W_i is final
+        if (i > 0) {  // (row 0: acc = -A_0j exactly, nothing to write)
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                const int mm = wm * 64 + jj * 16 + (lane & 15);
+                if (mm < mv && nn < nv) T[(size_t)mm + (size_t)nn * ldt] = -acc[ii][jj][r];
+              }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        dag_wait(colprog + i, colprog + i, i, i + 1, a.info, &s_wait);  // W_i final
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = d4v{0.0, 0.0, 0.0, 0.0};
+        dag_accum(acc, a.winv + (size_t)i * DT * DT, DT, mv, T, ldt, nv, mv / DTK, lds);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int mm = wm * 64 + jj * 16 + (lane & 15);
+              if (mm < mv && nn < nv) st_res<true>(&T[(size_t)mm + (size_t)nn * ldt], acc[ii][jj][r]);
+            }
+          }
+      }
+    }
+    DTRACE(1, 5);
+    dag_publish(pj, i + 1);
+    DTRACE(1, 6);
+  }
+  DTRACE(1, 7);
+}
+
+}  // namespace
+
+// Factor A (n x n, ld lda) in place and, when B != nullptr, B <- U^{-T} B (n x nrhs, ld ldb),
+// in one launch on ctx->stream.  Writes W_i into ctx->winv slots (block inverses for the
+// solves).  Returns 1 when the shape does not qualify (caller falls back), 0 when launched.
+int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb) {
+  if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || ((uintptr_t)dA & 127) || n > DT * 32767)
+    return 1;
+  if (dB && (nrhs <= 0 || ldb % 16 || ((uintptr_t)dB & 127) || nrhs > DT * 65535)) return 1;
+  const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
+  GPR_TRY(ensure_winv(ctx, n, DT));
+  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr) {
+    std::vector<unsigned> tasks;
+    tasks.reserve((size_t)nt * (nt + 1) / 2 + (size_t)nt * ntr);
+    for (int i = 0; i < nt; ++i) {
+      for (int j = i; j < nt; ++j) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
+      for (int c = 0; c < ntr; ++c) tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
+    }
+    if (ctx->dag_tasks) hipFree(ctx->dag_tasks);
+    ctx->dag_tasks = nullptr;
+    ctx->dag_nt = ctx->dag_ntr = -1;
+    HIP_TRY(ctx, hipMalloc((void**)&ctx->dag_tasks, tasks.size() * sizeof(unsigned)));
+    HIP_TRY(ctx, hipMemcpy(ctx->dag_tasks, tasks.data(), tasks.size() * sizeof(unsigned),
+                           hipMemcpyHostToDevice));
+    ctx->dag_ntasks = (int)tasks.size();
+    ctx->dag_nt = nt;
+    ctx->dag_ntr = ntr;
+  }
+  const size_t nsync = 2 + (size_t)nt + ntr;
+  if (ctx->dag_sync_cap < nsync) {
+    if (ctx->dag_sync) hipFree(ctx->dag_sync);
+    ctx->dag_sync = nullptr;
+    ctx->dag_sync_cap = 0;
+    HIP_TRY(ctx, hipMalloc((void**)&ctx->dag_sync, nsync * sizeof(int)));
+    ctx->dag_sync_cap = nsync;
+  }
+  HIP_TRY(ctx, hipMemsetAsync(ctx->dag_sync, 0, nsync * sizeof(int), ctx->stream));
+  if (ctx->ncu <= 0) {
+    hipDeviceProp_t prop;
+    HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
+    ctx->ncu = prop.multiProcessorCount;
+  }
+  DagArgs a{};
+  a.A = dA;
+  a.lda = (size_t)lda;
+  a.n = n;
+  a.nt = nt;
+  a.B = dB;
+  a.ldb = (size_t)(dB ? ldb : 0);
+  a.nrhs = dB ? nrhs : 0;
+  a.ntr = ntr;
+  a.winv = ctx->winv;
+  a.kglob = 0;
+  a.info = ctx->dinfo;
+  a.sync = ctx->dag_sync;
+  a.tasks = ctx->dag_tasks;
+  a.ntasks = ctx->dag_ntasks;
+  const int grid = std::min(ctx->dag_ntasks, ctx->ncu);
+  const double flops = (double)n * n * n / 3.0 + (double)n * n * (dB ? nrhs : 0);
+  {
+    TimerScope ts(ctx, TC_DAG, flops);
+    potrf_dag_kernel<<<grid, 256, 0, ctx->stream>>>(a);
+    LAUNCH_CHECK(ctx);
+  }
+  return 0;
+}

@@ -1,0 +1,282 @@
+// Diagonal-block factorisation device code, shared by potrf.hip (diag2_kernel: one launch per
+// 128-block of the blocked factorisation) and dag.hip (the F tasks of the persistent tile-DAG
+// factorisation).  One 256-thread workgroup factors a 128 x 128 block held in LDS (packed
+// upper) and writes U_bb and W_bb = U_bb^{-1}.
+#pragma once
+#include "common.hpp"
+
+#ifndef STAMP
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
+namespace {
+
+constexpr int DIAG_THREADS = 256;
+
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int pk(int r, int c) { return (c * (c + 1) >> 1) + r; }  // r <= c
+
+// 1/sqrt(x) to ~1 ulp: hardware rsq + one Newton step (shorter dependency chain than the
+// correctly-rounded sqrt + divide; this is the pivot of every sequential step)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x * y;
+  const double r = fma(-h, y, 0.5);
+  return fma(y, r, y);
+}
+
+// Global store of a result another workgroup of the SAME launch may read after a flag
+// (SC1: sc1 = write-through, the line leaves this XCD's L2 -- the MI355X guide's sc1
+// hand-off), or a plain store (results read only by later launches).
+template <bool SC1>
+__device__ __forceinline__ void st_res(double* p, double v) {
+  if constexpr (SC1)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
+// ---- diag kernel v2 (NB = 128, factor mode): no per-pivot workgroup barriers ------------
+// Per 32-row band sb (K0 = 32 sb, band = rows [K0, K0+32) x cols [K0, 128)):
+//   F1  the band is eliminated by whole waves WITHOUT barriers: a wave holds 64 columns of
+//       the band in registers (lane = column, register = row) and broadcasts the pivot row
+//       with v_readlane.  Every active wave carries the 32x32 diagonal block D in lanes 0-31
+//       (recomputed identically, so no wave waits for another) and 32 further columns in
+//       lanes 32-63: 32 strip columns (-> U = D^-T S), or, on the last active wave, the
+//       identity (-> D^-T, i.e. the rows of the 32x32 inverse Xd_sb for free).
+//   F3  trailing update of the rest of the block on MFMA (all waves).
+// Inverse W = U^-1 from U and the Xd: column half (J, jh) of W is a 16-column recurrence
+//   X_JJ = Xd_J,  X_IJ = -Xd_I sum_{K=I+1..J} U_IK X_KJ   (I = J-1 .. 0)
+// kept entirely in MFMA accumulators (D-layout register q = B operand of k-step q), one
+// wave per column half; W goes to the workspace slot with fire-and-forget stores.  No
+// global read-back and no barrier after a global store, so nothing waits on HBM latency
+// except the single batched load of the block.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+constexpr int D2_NB = 128;
+constexpr int D2_PK = D2_NB * (D2_NB + 1) / 2;  // packed 128x128 upper (66 KB)
+constexpr int D2_PB = 32 * 33 / 2;              // packed 32x32 upper
+
+// column half (J, jh) of W = U^-1 (see above); S = U packed upper (128), Xd = packed diag inverses
+template <int J, bool SC1>
+__device__ __forceinline__ void d2_inv_colhalf(int jh, const double* __restrict__ S,
+                                               const double (*__restrict__ Xd)[D2_PB],
+                                               double* __restrict__ winv, int kb, int lane) {
+  d4v X[J + 1][2];
+  const int col = 16 * jh + (lane & 15);  // column within block J
+#pragma unroll
+  for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * ih + (lane >> 4) + 4 * r;
+      const double v = Xd[J][pk(min(row, col), col)];
+      X[J][ih][r] = row <= col ? v : 0.0;
+    }
+#pragma unroll
+  for (int I = J - 1; I >= 0; --I) {
+    d4v T[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int K = I + 1; K <= J; ++K)
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int k = 32 * K + 4 * st + (lane >> 4);
+        const double b = X[K][st >> 2][st & 3];
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {
+          const double a = S[pk(32 * I + 16 * ih + (lane & 15), k)];
+          T[ih] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, T[ih], 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int ih = 0; ih < 2; ++ih) {
+      d4v acc = {0.0, 0.0, 0.0, 0.0};
+      const int i = 16 * ih + (lane & 15);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int m = 4 * st + (lane >> 4);
+        const double xv = Xd[I][pk(min(i, m), m)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(i <= m ? xv : 0.0, T[st >> 2][st & 3], acc, 0, 0, 0);
+      }
+      X[I][ih] = -acc;
+    }
+  }
+  const int gc = 32 * J + col;
+#pragma unroll
+  for (int I = 0; I < 4; ++I)
+#pragma unroll
+    for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = 32 * I + 16 * ih + (lane >> 4) + 4 * r;
+        const double v = (I <= J) ? X[I <= J ? I : 0][ih][r] : 0.0;
+        st_res<SC1>(&winv[gr + (size_t)gc * 128], (gr < kb && gc < kb) ? v : 0.0);
+      }
+}
+
+// S <- the upper triangle of the kb x kb block at Ab (identity padding beyond kb), packed.
+// Batched loads, 4 x 16 in flight: thread t owns row r = t % 128 of columns c0 + 2e.  Clamped
+// addresses + select: every load is issued unconditionally (a branch around a load makes the
+// compiler drain vmcnt on the other path, serialising the batch).
+__device__ __forceinline__ void diag2_load(double* __restrict__ S, const double* __restrict__ Ab,
+                                           size_t lda, int kb) {
+  constexpr int PER = D2_NB * D2_NB / DIAG_THREADS;
+  const int tid = threadIdx.x;
+  const int r = tid & (D2_NB - 1), c0 = tid >> 7;
+  const double* src = Ab + min(r, kb - 1);
+#pragma unroll 1
+  for (int e0 = 0; e0 < PER; e0 += 16) {
+    double v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = src[(size_t)min(c0 + 2 * (e0 + e), kb - 1) * lda];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int c = c0 + 2 * (e0 + e);
+      if (r <= c) S[pk(r, c)] = (c < kb) ? v[e] : ((r == c) ? 1.0 : 0.0);
+    }
+  }
+}
+
+// Factor the block in S (packed upper, loaded, identity padding beyond kb; the caller has
+// synchronised after filling it), write U to Ab (upper part only) and W = U^{-1} to winv
+// (128 x 128, zero outside kb x kb).  Returns 0, or the global order (kglob + row + 1) of
+// the first non-positive pivot -- then nothing is written.  Uniform across the workgroup.
+// Xd: 4 x D2_PB doubles of LDS; fail: one int of LDS.
+template <bool SC1>
+__device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__restrict__ Xd)[D2_PB],
+                                          int* fail, double* __restrict__ Ab, size_t lda, int kb,
+                                          int kglob, double* __restrict__ winv) {
+  constexpr int NB = D2_NB, PER = NB * NB / DIAG_THREADS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wv == 0) *fail = 0;  // (wave-uniform branch)
+  __syncthreads();
+#pragma unroll 1
+  for (int sb = 0; sb < 4; ++sb) {
+    const int K0 = 32 * sb, W = NB - K0;
+    const int nsw = (W - 32) / 32;  // waves carrying strip columns; wave nsw carries I
+    if (wv <= nsw) {
+      const bool dl = lane < 32;
+      const bool il = !dl && wv == nsw;
+      const int c = dl ? lane : 32 + 32 * wv + (lane - 32);  // band column (D / strip)
+      const int q = lane - 32;                                // identity column
+      double x[32];
+#pragma unroll
+      for (int r = 0; r < 32; ++r) {
+        const int cc = il ? r : c;  // any valid address for identity lanes
+        const double sv = S[pk(K0 + min(r, cc), K0 + cc)];
+        x[r] = il ? (r == q ? 1.0 : 0.0) : ((dl && r > lane) ? 0.0 : sv);
+      }
+      int bad = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const double piv = readlane_d(x[j], j);
+        bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
+        const double ri = rsqrt_nr(piv);
+        const double u = piv * ri;
+        const double xs = x[j] * ri;
+        x[j] = dl ? (lane == j ? u : (lane < j ? x[j] : xs)) : xs;
+        // row j to every lane in groups of 8: the readlanes of a group are issued back to
+        // back (their latency overlaps), then the group's FMAs; sched barriers keep the
+        // compiler from hoisting a whole step's readlanes (SGPR pressure)
+#pragma unroll
+        for (int i0 = j + 1; i0 < 32; i0 += 8) {
+          double u8[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (i0 + t < 32) u8[t] = readlane_d(x[j], i0 + t);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (i0 + t < 32) x[i0 + t] = fma(-u8[t], x[j], x[i0 + t]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (dl) {
+        if (wv == 0) {
+#pragma unroll
+          for (int r = 0; r < 32; ++r)
+            if (r <= lane) S[pk(K0 + r, K0 + lane)] = x[r];
+        }
+      } else if (il) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r)
+          if (r >= q) Xd[sb][pk(q, r)] = x[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) S[pk(K0 + r, K0 + c)] = x[r];
+      }
+      if (wv == 0 && lane == 0 && bad) *fail = kglob + K0 + bad;
+    }
+    __syncthreads();
+    if (sb == 0) STAMP(5);
+    const int f = __builtin_amdgcn_readfirstlane(*fail);  // uniform branch around barriers
+    if (f) return f;
+    const int R = W - 32;
+    if (R <= 0) break;
+    // F3: U(r, c) -= sum_p U(K0+p, r) U(K0+p, c) for K0+32 <= r <= c < NB, on MFMA
+    {
+      const int nt = R / 16, B0 = K0 + 32;
+      const int ntile = nt * (nt + 1) / 2;
+      for (int t = wv; t < ntile; t += DIAG_THREADS / 64) {
+        int tj = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+        while ((tj + 1) * (tj + 2) / 2 <= t) ++tj;
+        while (tj * (tj + 1) / 2 > t) --tj;
+        const int ti = t - tj * (tj + 1) / 2;
+        const int r0 = B0 + 16 * ti, q0 = B0 + 16 * tj;
+        double av[8], bv[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const int p = K0 + 4 * kk + (lane >> 4);
+          av[kk] = S[pk(p, r0 + (lane & 15))];
+          bv[kk] = S[pk(p, q0 + (lane & 15))];
+        }
+        d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], bv[kk], acc, 0, 0, 0);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int r = r0 + (lane >> 4) + 4 * qq, c = q0 + (lane & 15);
+          if (r <= c) S[pk(r, c)] -= acc[qq];
+        }
+      }
+    }
+    __syncthreads();
+    if (sb == 0) STAMP(6);
+  }
+  STAMP(2);
+  // U back to global (fire-and-forget; nothing below waits for these stores)
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int idx = tid + e * DIAG_THREADS;
+    const int r = idx % NB, c = idx / NB;
+    if (r < kb && c < kb && r <= c) st_res<SC1>(&Ab[(size_t)r + (size_t)c * lda], S[pk(r, c)]);
+  }
+  // W = U^-1, one wave per column half (MFMA work 144 / 144 / 112 / 112)
+  if (wv == 0) {
+    d2_inv_colhalf<3, SC1>(0, S, Xd, winv, kb, lane);
+  } else if (wv == 1) {
+    d2_inv_colhalf<3, SC1>(1, S, Xd, winv, kb, lane);
+  } else {
+    const int jh = wv - 2;
+    d2_inv_colhalf<2, SC1>(jh, S, Xd, winv, kb, lane);
+    d2_inv_colhalf<1, SC1>(jh, S, Xd, winv, kb, lane);
+    d2_inv_colhalf<0, SC1>(jh, S, Xd, winv, kb, lane);
+  }
+  STAMP(4);
+  return 0;
+}
+
+}  // namespace

@@ -169,6 +169,9 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     if (q > 0) ctx->cv_streams = std::min(ctx->cv_streams, q);
   }
   if (const char* e = getenv("GPR_PANEL")) ctx->panel_mode = atoi(e);
+  if (const char* e = getenv("GPR_DAG")) ctx->dag_mode = atoi(e);
+  if (const char* e = getenv("GPR_DAG_NMIN")) ctx->dag_nmin = atoi(e);
+  if (const char* e = getenv("GPR_DAG_NMAX")) ctx->dag_nmax = atoi(e);
   if (const char* e = getenv("GPR_INV_STRIP_MIN")) ctx->inv_strip_min = atoi(e);
   if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
@@ -233,6 +236,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dscr_wt) hipFree(ctx->dscr_wt);
   if (ctx->sdiag) hipStreamDestroy(ctx->sdiag);
   if (ctx->smain) hipStreamDestroy(ctx->smain);
+  if (ctx->dag_tasks) hipFree(ctx->dag_tasks);
+  if (ctx->dag_sync) hipFree(ctx->dag_sync);
   if (ctx->winv) hipFree(ctx->winv);
   if (ctx->dinfo) hipFree(ctx->dinfo);
   if (ctx->dexptab) hipFree(ctx->dexptab);

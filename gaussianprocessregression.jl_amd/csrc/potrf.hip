@@ -33,9 +33,9 @@ extern "C" void gpr_debug_diag_stamps(unsigned long long* out) {
   } while (0)
 #endif
 
-namespace {
+#include "diag_block.hpp"
 
-constexpr int DIAG_THREADS = 256;
+namespace {
 
 // ---- blocked diagonal-block kernel ------------------------------------------------------
 // Factor (mode 1) / only invert (mode 0) one NB x NB diagonal block, blocked by SB = 32:
@@ -56,24 +56,6 @@ constexpr int DIAG_THREADS = 256;
 // full-CU footprint it waited ~0.7 ms per call for a CU to drain (measured).  Off-diagonal
 // blocks of U^{-1} go straight to the workspace slot and are re-read by B2 with one batched
 // prefetch per tile.  Padding beyond kb is the identity.
-typedef double d4v __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void wave_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ int pk(int r, int c) { return (c * (c + 1) >> 1) + r; }  // r <= c
-
-// 1/sqrt(x) to ~1 ulp: hardware rsq + one Newton step (shorter dependency chain than the
-// correctly-rounded sqrt + divide; this is the pivot of every sequential step)
-__device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  const double h = 0.5 * x * y;
-  const double r = fma(-h, y, 0.5);
-  return fma(y, r, y);
-}
 
 template <int NB>
 __device__ __forceinline__ void diag_block_body(double* __restrict__ A, size_t lda, int n,
@@ -378,239 +360,33 @@ __global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __r
   diag_block_body<NB>(A, lda, n, kglob, info, winv, mode, blockIdx.x);
 }
 
-// ---- diag kernel v2 (NB = 128, factor mode): no per-pivot workgroup barriers ------------
-// Per 32-row band sb (K0 = 32 sb, band = rows [K0, K0+32) x cols [K0, 128)):
-//   F1  the band is eliminated by whole waves WITHOUT barriers: a wave holds 64 columns of
-//       the band in registers (lane = column, register = row) and broadcasts the pivot row
-//       with v_readlane.  Every active wave carries the 32x32 diagonal block D in lanes 0-31
-//       (recomputed identically, so no wave waits for another) and 32 further columns in
-//       lanes 32-63: 32 strip columns (-> U = D^-T S), or, on the last active wave, the
-//       identity (-> D^-T, i.e. the rows of the 32x32 inverse Xd_sb for free).
-//   F3  trailing update of the rest of the block on MFMA (all waves).
-// Inverse W = U^-1 from U and the Xd: column half (J, jh) of W is a 16-column recurrence
-//   X_JJ = Xd_J,  X_IJ = -Xd_I sum_{K=I+1..J} U_IK X_KJ   (I = J-1 .. 0)
-// kept entirely in MFMA accumulators (D-layout register q = B operand of k-step q), one
-// wave per column half; W goes to the workspace slot with fire-and-forget stores.  No
-// global read-back and no barrier after a global store, so nothing waits on HBM latency
-// except the single batched load of the block.
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
-constexpr int D2_PB = 32 * 33 / 2;  // packed 32x32 upper
-
-// column half (J, jh) of W = U^-1 (see above); S = U packed upper (128), Xd = packed diag inverses
-template <int J>
-__device__ __forceinline__ void d2_inv_colhalf(int jh, const double* __restrict__ S,
-                                               const double (*__restrict__ Xd)[D2_PB],
-                                               double* __restrict__ winv, int kb, int lane) {
-  d4v X[J + 1][2];
-  const int col = 16 * jh + (lane & 15);  // column within block J
-#pragma unroll
-  for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 16 * ih + (lane >> 4) + 4 * r;
-      const double v = Xd[J][pk(min(row, col), col)];
-      X[J][ih][r] = row <= col ? v : 0.0;
-    }
-#pragma unroll
-  for (int I = J - 1; I >= 0; --I) {
-    d4v T[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-#pragma unroll
-    for (int K = I + 1; K <= J; ++K)
-#pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        const int k = 32 * K + 4 * st + (lane >> 4);
-        const double b = X[K][st >> 2][st & 3];
-#pragma unroll
-        for (int ih = 0; ih < 2; ++ih) {
-          const double a = S[pk(32 * I + 16 * ih + (lane & 15), k)];
-          T[ih] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, T[ih], 0, 0, 0);
-        }
-      }
-#pragma unroll
-    for (int ih = 0; ih < 2; ++ih) {
-      d4v acc = {0.0, 0.0, 0.0, 0.0};
-      const int i = 16 * ih + (lane & 15);
-#pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        const int m = 4 * st + (lane >> 4);
-        const double xv = Xd[I][pk(min(i, m), m)];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(i <= m ? xv : 0.0, T[st >> 2][st & 3], acc, 0, 0, 0);
-      }
-      X[I][ih] = -acc;
-    }
-  }
-  const int gc = 32 * J + col;
-#pragma unroll
-  for (int I = 0; I < 4; ++I)
-#pragma unroll
-    for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gr = 32 * I + 16 * ih + (lane >> 4) + 4 * r;
-        const double v = (I <= J) ? X[I <= J ? I : 0][ih][r] : 0.0;
-        winv[gr + (size_t)gc * 128] = (gr < kb && gc < kb) ? v : 0.0;
-      }
-}
-
+// One 128-block (factor mode) per launch; the body is diag_block.hpp's diag2_core.
 // <= 256 registers per wave: the kernel must fit on a CU beside one running trailing-update
 // workgroup (224 registers per wave), or it waits for the CU to drain
+// The block lives in DYNAMIC LDS (DIAG2_LDS bytes at launch): with 84 KB of static LDS the
+// compiler sees that two workgroups cannot share a CU, drops the 2-per-CU register target and
+// allocates ~310 registers per wave, and the kernel would no longer fit beside a trailing-
+// update workgroup (224 registers per wave).
+constexpr size_t DIAG2_LDS = sizeof(double) * (D2_PK + 4 * D2_PB) + 16;
 __global__ __launch_bounds__(DIAG_THREADS, 2) void diag2_kernel(double* __restrict__ A, size_t lda,
                                                                 int n, int kglob,
                                                                 int* __restrict__ info,
                                                                 double* __restrict__ winv) {
-  constexpr int NB = 128, PK = NB * (NB + 1) / 2, PER = NB * NB / DIAG_THREADS;
-  __shared__ double S[PK];           // U, packed upper (66 KB)
-  __shared__ double Xd[4][D2_PB];    // diagonal 32x32 blocks of U^-1, packed upper (17 KB)
-  __shared__ int fail;
+  extern __shared__ double dsm[];
+  double* S = dsm;                                               // U, packed upper (66 KB)
+  double(*Xd)[D2_PB] = reinterpret_cast<double(*)[D2_PB]>(dsm + D2_PK);  // U^-1 diag blocks
+  int* fail = reinterpret_cast<int*>(dsm + D2_PK + 4 * D2_PB);
   if (*info != 0) return;
+  // this latency-bound chain shares CUs with the MFMA-saturating trailing update: take
+  // issue priority over the co-resident GEMM waves
   __builtin_amdgcn_s_setprio(3);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kb = min(NB, n - kglob);
+  const int kb = min(D2_NB, n - kglob);
   double* Ab = A + (size_t)kglob + (size_t)kglob * lda;
   STAMP(0);
-  // batched loads of the upper block (identity padding beyond kb), 4 x 16 in flight.  Thread
-  // t owns row r = t % 128 of columns c0 + 2e.  Clamped addresses + select: every load is
-  // issued unconditionally (a branch around a load makes the compiler drain vmcnt on the
-  // other path, serialising the batch).
-  {
-    const int r = tid & (NB - 1), c0 = tid >> 7;
-    const double* src = Ab + min(r, kb - 1);
-#pragma unroll 1
-    for (int e0 = 0; e0 < PER; e0 += 16) {
-      double v[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = src[(size_t)min(c0 + 2 * (e0 + e), kb - 1) * lda];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int c = c0 + 2 * (e0 + e);
-        if (r <= c) S[pk(r, c)] = (c < kb) ? v[e] : ((r == c) ? 1.0 : 0.0);
-      }
-    }
-  }
-  if (tid == 0) fail = 0;
-  __syncthreads();
+  diag2_load(S, Ab, lda, kb);
   STAMP(1);
-#pragma unroll 1
-  for (int sb = 0; sb < 4; ++sb) {
-    const int K0 = 32 * sb, W = NB - K0;
-    const int nsw = (W - 32) / 32;  // waves carrying strip columns; wave nsw carries I
-    if (wv <= nsw) {
-      const bool dl = lane < 32;
-      const bool il = !dl && wv == nsw;
-      const int c = dl ? lane : 32 + 32 * wv + (lane - 32);  // band column (D / strip)
-      const int q = lane - 32;                                // identity column
-      double x[32];
-#pragma unroll
-      for (int r = 0; r < 32; ++r) {
-        const int cc = il ? r : c;  // any valid address for identity lanes
-        const double sv = S[pk(K0 + min(r, cc), K0 + cc)];
-        x[r] = il ? (r == q ? 1.0 : 0.0) : ((dl && r > lane) ? 0.0 : sv);
-      }
-      int bad = 0;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const double piv = readlane_d(x[j], j);
-        bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
-        const double ri = rsqrt_nr(piv);
-        const double u = piv * ri;
-        const double xs = x[j] * ri;
-        x[j] = dl ? (lane == j ? u : (lane < j ? x[j] : xs)) : xs;
-        // row j to every lane in groups of 8: the readlanes of a group are issued back to
-        // back (their latency overlaps), then the group's FMAs; sched barriers keep the
-        // compiler from hoisting a whole step's readlanes (SGPR pressure)
-#pragma unroll
-        for (int i0 = j + 1; i0 < 32; i0 += 8) {
-          double u8[8];
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            if (i0 + t < 32) u8[t] = readlane_d(x[j], i0 + t);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            if (i0 + t < 32) x[i0 + t] = fma(-u8[t], x[j], x[i0 + t]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (dl) {
-        if (wv == 0) {
-#pragma unroll
-          for (int r = 0; r < 32; ++r)
-            if (r <= lane) S[pk(K0 + r, K0 + lane)] = x[r];
-        }
-      } else if (il) {
-#pragma unroll
-        for (int r = 0; r < 32; ++r)
-          if (r >= q) Xd[sb][pk(q, r)] = x[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 32; ++r) S[pk(K0 + r, K0 + c)] = x[r];
-      }
-      if (wv == 0 && lane == 0 && bad) fail = kglob + K0 + bad;
-    }
-    __syncthreads();
-    if (sb == 0) STAMP(5);
-    if (fail) {
-      if (tid == 0) *info = fail;
-      return;
-    }
-    const int R = W - 32;
-    if (R <= 0) break;
-    // F3: U(r, c) -= sum_p U(K0+p, r) U(K0+p, c) for K0+32 <= r <= c < NB, on MFMA
-    {
-      const int nt = R / 16, B0 = K0 + 32;
-      const int ntile = nt * (nt + 1) / 2;
-      for (int t = wv; t < ntile; t += DIAG_THREADS / 64) {
-        int tj = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-        while ((tj + 1) * (tj + 2) / 2 <= t) ++tj;
-        while (tj * (tj + 1) / 2 > t) --tj;
-        const int ti = t - tj * (tj + 1) / 2;
-        const int r0 = B0 + 16 * ti, q0 = B0 + 16 * tj;
-        double av[8], bv[8];
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int p = K0 + 4 * kk + (lane >> 4);
-          av[kk] = S[pk(p, r0 + (lane & 15))];
-          bv[kk] = S[pk(p, q0 + (lane & 15))];
-        }
-        d4v acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], bv[kk], acc, 0, 0, 0);
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int r = r0 + (lane >> 4) + 4 * qq, c = q0 + (lane & 15);
-          if (r <= c) S[pk(r, c)] -= acc[qq];
-        }
-      }
-    }
-    __syncthreads();
-    if (sb == 0) STAMP(6);
-  }
-  STAMP(2);
-  // U back to global (fire-and-forget; nothing below waits for these stores)
-#pragma unroll
-  for (int e = 0; e < PER; ++e) {
-    const int idx = tid + e * DIAG_THREADS;
-    const int r = idx % NB, c = idx / NB;
-    if (r < kb && c < kb && r <= c) Ab[(size_t)r + (size_t)c * lda] = S[pk(r, c)];
-  }
-  // W = U^-1, one wave per column half (MFMA work 144 / 144 / 112 / 112)
-  if (wv == 0) {
-    d2_inv_colhalf<3>(0, S, Xd, winv, kb, lane);
-  } else if (wv == 1) {
-    d2_inv_colhalf<3>(1, S, Xd, winv, kb, lane);
-  } else {
-    const int jh = wv - 2;
-    d2_inv_colhalf<2>(jh, S, Xd, winv, kb, lane);
-    d2_inv_colhalf<1>(jh, S, Xd, winv, kb, lane);
-    d2_inv_colhalf<0>(jh, S, Xd, winv, kb, lane);
-  }
-  STAMP(4);
+  const int f = diag2_core<false>(S, Xd, fail, Ab, lda, kb, kglob, winv);
+  if (f && threadIdx.x == 0) *info = f;
 #ifdef GPR_DIAG_STAMPS
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     g_diag_stamps[3] = g_diag_stamps[2];
@@ -1215,7 +991,8 @@ int launch_diag(gpr_ctx* ctx, double* A, int lda, int n, int kglob, double* winv
   static const bool v1 = getenv("GPR_DIAG_V1") != nullptr;
   if (fake && mode == 1) mode = 3;
   if (nb == 128 && mode == 1 && !v1 && nblocks == 1)
-    diag2_kernel<<<1, DIAG_THREADS, 0, ctx->ls>>>(A, (size_t)lda, n, kglob, ctx->dinfo, winv);
+    diag2_kernel<<<1, DIAG_THREADS, DIAG2_LDS, ctx->ls>>>(A, (size_t)lda, n, kglob, ctx->dinfo,
+                                                       winv);
   else if (nb == 128)
     diag_block_kernel<128><<<nblocks, DIAG_THREADS, 0, ctx->ls>>>(A, (size_t)lda, n, kglob,
                                                                       ctx->dinfo, winv, mode);
@@ -1860,6 +1637,31 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap,
                        (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));
     GPR_TRY(ensure_buf(ctx, &ctx->dpanel_rhs, &ctx->panel_rhs_cap, (size_t)nb2 * rhs->nrhs));
+  }
+  if (ctx->dag_mode && n >= ctx->dag_nmin && n <= ctx->dag_nmax &&
+      (!rhs || (!rhs->gram && !rhs->lower_rhs))) {
+    // one persistent launch: tiles handed between workgroups by progress counters
+    HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
+    const int rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
+                                    rhs ? rhs->ldb : 0);
+    if (rc < 0) return rc;
+    if (rc == 0) {
+      int hinfo = 0;
+      HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      if (hinfo < 0)
+        return set_err(ctx, GPR_E_HIP, "tile-DAG factorisation: a dependency wait timed out");
+      if (info) *info = hinfo;
+      if (hinfo == 0) {
+        ctx->fac_valid = true;
+        ctx->fac_ptr = dA;
+        ctx->fac_n = n;
+        ctx->fac_ld = lda;
+        ctx->fac_nb = nb;
+      }
+      return 0;
+    }
   }
   hipStream_t user = ctx->stream;
   hipStream_t s0 = ctx->smain ? ctx->smain : ctx->stream, s1 = ctx->stream2;

@@ -244,6 +244,38 @@ def test_potrf_not_posdef_info_later_panels(j, panel_sq, monkeypatch):
     assert info == info_ref == j + 1
 
 
+@pytest.mark.parametrize("n", [16, 128, 144, 256, 400, 1040, 2064, 4112])
+def test_potrf_dag(n, monkeypatch):
+    """Persistent tile-DAG factorisation (dag.hip, GPR_DAG=1): one launch, tiles handed
+    between workgroups by progress counters; ragged last tile (n % 128 != 0), upper factor,
+    lower triangle untouched, block inverses usable by the solves."""
+    monkeypatch.setenv("GPR_DAG", "1")
+    ctx = G.Context(0)
+    A = _spd(n, seed=n + 7)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    R = ctx.host(dA)
+    U = sla.cholesky(A, lower=False)
+    assert relnorm(np.triu(R), U) < 1e-12
+    assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
+    B = np.random.default_rng(4).random((n, 2))
+    dB = ctx.colmajor(B)
+    assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                      ctypes.c_void_p(dB.data_ptr()), 2, n) == 0
+    assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
+
+
+@pytest.mark.parametrize("j", [0, 5, 127, 128, 200, 1000, 1039])
+def test_potrf_dag_not_posdef_info(j, monkeypatch):
+    monkeypatch.setenv("GPR_DAG", "1")
+    ctx = G.Context(0)
+    A = _spd(1040, seed=2)
+    A[j, j] = -1.0
+    _, info = _dev_potrf(ctx, A)
+    _, info_ref = sla.lapack.dpotrf(A, lower=0)
+    assert info == info_ref == j + 1
+
+
 @pytest.mark.parametrize("j", [0, 5, 127, 128, 200])
 def test_potrf_not_posdef_info(j):
     """Non-PD input: info = order of the failing leading minor (dpotrf / PosDefException)."""

@@ -255,7 +255,7 @@ def main():
         stg[nm] = e[i].elapsed_time(e[i + 1])
     unfused_ms = sum(stg.values())
     cls = {}
-    for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other", "gemm_pipe"]):
+    for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other", "gemm_pipe", "dag"]):
         ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
         lib.gpr_timing_get(ctx.h, c, ctypes.byref(ms), ctypes.byref(ln), ctypes.byref(fl))
         cls[nm] = (ms.value, ln.value, fl.value)
@@ -294,6 +294,9 @@ def main():
             "unfused_job_ms": unfused_ms,
             "instrumented_step_ms": fused_ms,
             "syrk_TFLOPs": cls["syrk"][2] / (cls["syrk"][0] * 1e-3) / 1e12 if cls["syrk"][0] else None,
+            # the persistent tile-DAG launch (whole factorisation at N <= 16384, else the tail)
+            "dag_ms": cls["dag"][0], "dag_launches": cls["dag"][1],
+            "dag_TFLOPs": cls["dag"][2] / (cls["dag"][0] * 1e-3) / 1e12 if cls["dag"][0] else None,
             "roofline": {
                 "kernel": " + ".join(DOMINANT_KERNELS),
                 "bound": "mfma",

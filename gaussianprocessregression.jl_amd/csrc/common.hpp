@@ -70,9 +70,14 @@ struct gpr_ctx {
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   // persistent tile-DAG factorisation (dag.hip): 0 off, 1 on for dag_nmin <= n <= dag_nmax
-  // (GPR_DAG, GPR_DAG_NMIN, GPR_DAG_NMAX); the task list is cached per (tiles, rhs tiles)
-  int dag_mode = 0;
-  int dag_nmin = 0, dag_nmax = 1 << 30;
+  // (GPR_DAG, GPR_DAG_NMIN, GPR_DAG_NMAX); the task list is cached per (tiles, rhs tiles).
+  // Measured (POTRF alone): N = 8192 9.3 -> 6.9 ms, 16384 34.5 -> 29.6; at 32768 the DAG's
+  // tile tasks (53 TF/s) lose to the blocked trailing SYRKs (61), so larger factorisations
+  // keep the blocked path and hand only their chain-bound tail to the DAG.
+  int dag_mode = 1;
+  int dag_nmin = 0, dag_nmax = 16384;
+  int dag_tail = 12288;  // blocked factorisations hand their last <= dag_tail columns to the
+                         // DAG (GPR_DAG_TAIL; 0 = off): C3 POTRF 193.5 -> 188.3 ms
   unsigned* dag_tasks = nullptr;
   int dag_ntasks = 0, dag_nt = -1, dag_ntr = -1;
   int* dag_sync = nullptr;
@@ -217,7 +222,8 @@ struct RhsSpec {
   int ldg;
 };
 // one-launch tile-DAG factorisation (+ B <- U^{-T} B); 1 = shape not eligible, 0 = launched
-int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb);
+int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
+                     int kglob, hipStream_t st);
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
                const RhsSpec* rhs = nullptr);
 int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);

@@ -51,9 +51,20 @@ extern "C" void gpr_debug_dag_trace(int* out, void* stream) {
                            hipMemcpyDeviceToHost, (hipStream_t)stream);
   hipStreamSynchronize((hipStream_t)stream);
 }
+// phase timers (100 MHz realtime ticks), summed per workgroup into trace slots 2..7
+#define PROF(var, ...)                                  \
+  do {                                                  \
+    const unsigned long long _t0 = __builtin_amdgcn_s_memrealtime(); \
+    __VA_ARGS__;                                        \
+    var += __builtin_amdgcn_s_memrealtime() - _t0;      \
+  } while (0)
 #else
 #define DTRACE(slot, v) \
   do {                  \
+  } while (0)
+#define PROF(var, ...) \
+  do {                 \
+    __VA_ARGS__;       \
   } while (0)
 #endif
 
@@ -257,6 +268,11 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
   const int wm = w & 1, wn = w >> 1;
   int* colprog = a.sync + 2;
   int* rhsprog = colprog + a.nt;
+  unsigned long long p_wait = 0, p_acc = 0, p_fac = 0, p_tri = 0, p_all = 0, p_n = 0;
+  (void)p_wait; (void)p_acc; (void)p_fac; (void)p_tri; (void)p_all; (void)p_n;
+#ifdef DAG_TRACE
+  const unsigned long long p_start = __builtin_amdgcn_s_memrealtime();
+#endif
   for (;;) {
     if (w == 0) {  // one ticket: lane 0 adds 1, the other lanes 0 (a wave-wide atomic)
       const int tk = atomicAdd(&a.sync[0], lane == 0 ? 1 : 0);
@@ -305,9 +321,10 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
       DTRACE(1, 2);
       int done = 0;
       while (done < i) {
-        const int r = dag_wait(colprog + i, pj, done, i, a.info, &s_wait);
-        dag_accum(acc, Pcol + (size_t)done * DT, a.lda, mv, Qcol + (size_t)done * DT, ldt, nv,
-                  (r - done) * (DT / DTK), lds);
+        int r = 0;
+        PROF(p_wait, r = dag_wait(colprog + i, pj, done, i, a.info, &s_wait));
+        PROF(p_acc, dag_accum(acc, Pcol + (size_t)done * DT, a.lda, mv, Qcol + (size_t)done * DT,
+                              ldt, nv, (r - done) * (DT / DTK), lds));
         done = r;
       }
       if (diag) {
@@ -326,7 +343,8 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
           }
         __syncthreads();
         DTRACE(1, 3);
-        const int f = dag_factor(S, T, a.lda, mv, a.kglob + i * DT, a.winv + (size_t)i * DT * DT);
+        int f = 0;
+        PROF(p_fac, f = dag_factor(S, T, a.lda, mv, a.kglob + i * DT, a.winv + (size_t)i * DT * DT));
         if (f && w == 0) atomicCAS(a.info, 0, f);
         DTRACE(1, 4);
       } else {
@@ -347,12 +365,12 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        dag_wait(colprog + i, colprog + i, i, i + 1, a.info, &s_wait);  // W_i final
+        PROF(p_wait, dag_wait(colprog + i, colprog + i, i, i + 1, a.info, &s_wait));  // W_i final
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = d4v{0.0, 0.0, 0.0, 0.0};
-        dag_accum(acc, a.winv + (size_t)i * DT * DT, DT, mv, T, ldt, nv, mv / DTK, lds);
+        PROF(p_tri, dag_accum(acc, a.winv + (size_t)i * DT * DT, DT, mv, T, ldt, nv, mv / DTK, lds));
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -369,8 +387,18 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
     DTRACE(1, 5);
     dag_publish(pj, i + 1);
     DTRACE(1, 6);
+    ++p_n;
   }
   DTRACE(1, 7);
+#ifdef DAG_TRACE
+  p_all = __builtin_amdgcn_s_memrealtime() - p_start;
+  DTRACE(2, (int)p_wait);
+  DTRACE(3, (int)p_acc);
+  DTRACE(4, (int)p_fac);
+  DTRACE(5, (int)p_tri);
+  DTRACE(6, (int)p_all);
+  DTRACE(7, (int)p_n);
+#endif
 }
 
 }  // namespace
@@ -378,12 +406,16 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
 // Factor A (n x n, ld lda) in place and, when B != nullptr, B <- U^{-T} B (n x nrhs, ld ldb),
 // in one launch on ctx->stream.  Writes W_i into ctx->winv slots (block inverses for the
 // solves).  Returns 1 when the shape does not qualify (caller falls back), 0 when launched.
-int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb) {
-  if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || ((uintptr_t)dA & 127) || n > DT * 32767)
+// kglob: global index of A's first row/column (the trailing matrix of a blocked factorisation:
+// block inverses go to winv slots kglob/128 + i, pivot orders are global); st: the stream.
+int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
+                     int kglob, hipStream_t st) {
+  if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || ((uintptr_t)dA & 127) || n > DT * 32767 ||
+      kglob % DT)
     return 1;
   if (dB && (nrhs <= 0 || ldb % 16 || ((uintptr_t)dB & 127) || nrhs > DT * 65535)) return 1;
   const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
-  GPR_TRY(ensure_winv(ctx, n, DT));
+  GPR_TRY(ensure_winv(ctx, kglob + n, DT));
   if (ctx->dag_nt != nt || ctx->dag_ntr != ntr) {
     std::vector<unsigned> tasks;
     tasks.reserve((size_t)nt * (nt + 1) / 2 + (size_t)nt * ntr);
@@ -409,7 +441,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     HIP_TRY(ctx, hipMalloc((void**)&ctx->dag_sync, nsync * sizeof(int)));
     ctx->dag_sync_cap = nsync;
   }
-  HIP_TRY(ctx, hipMemsetAsync(ctx->dag_sync, 0, nsync * sizeof(int), ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(ctx->dag_sync, 0, nsync * sizeof(int), st));
   if (ctx->ncu <= 0) {
     hipDeviceProp_t prop;
     HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
@@ -424,8 +456,8 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   a.ldb = (size_t)(dB ? ldb : 0);
   a.nrhs = dB ? nrhs : 0;
   a.ntr = ntr;
-  a.winv = ctx->winv;
-  a.kglob = 0;
+  a.winv = ctx->winv + (size_t)(kglob / DT) * DT * DT;
+  a.kglob = kglob;
   a.info = ctx->dinfo;
   a.sync = ctx->dag_sync;
   a.tasks = ctx->dag_tasks;
@@ -433,8 +465,11 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   const int grid = std::min(ctx->dag_ntasks, ctx->ncu);
   const double flops = (double)n * n * n / 3.0 + (double)n * n * (dB ? nrhs : 0);
   {
+    hipStream_t ls = ctx->ls;
+    ctx->ls = st;  // TimerScope records on ctx->ls
     TimerScope ts(ctx, TC_DAG, flops);
-    potrf_dag_kernel<<<grid, 256, 0, ctx->stream>>>(a);
+    potrf_dag_kernel<<<grid, 256, 0, st>>>(a);
+    ctx->ls = ls;
     LAUNCH_CHECK(ctx);
   }
   return 0;

@@ -1643,7 +1643,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     // one persistent launch: tiles handed between workgroups by progress counters
     HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
     const int rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
-                                    rhs ? rhs->ldb : 0);
+                                    rhs ? rhs->ldb : 0, 0, ctx->stream);
     if (rc < 0) return rc;
     if (rc == 0) {
       int hinfo = 0;
@@ -1724,8 +1724,31 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   hipEvent_t ev_p = sync_event(ctx, ev++);
   hipEvent_t ev_b = nullptr;
   if (!rc && hipEventRecord(ev_p, s1) != hipSuccess) rc = GPR_E_HIP;
+  // tail hand-off: once the trailing matrix is <= dag_tail, ONE SYRK applies panel s to all of
+  // it and the tile-DAG factors it (the blocked path is chain-bound there)
+  const bool tail_ok = ctx->dag_tail > 0 && !rhs && nb == 128 && lda % 16 == 0 &&
+                       ((uintptr_t)dA & 127) == 0 && n % 16 == 0 && !sqp;
+  bool tail_done = false;
   for (int k = 0; !rc && k + nb2 < n; k += nb2) {
     const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
+    if (tail_ok && n - kend <= ctx->dag_tail) {
+      ctx->ls = s0;
+      if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
+      GemmArgs b{};
+      b.P = dA + k + (size_t)kend * lda; b.ldp = lda;
+      b.Q = b.P; b.ldq = lda;
+      b.C = dA + kend + (size_t)kend * lda; b.ldc = lda;
+      b.M = n - kend; b.N = n - kend; b.K = kend - k;
+      b.alpha = -1.0; b.beta = 1.0;
+      b.upper = 1;
+      b.info = ctx->dinfo;
+      if ((rc = launch_gemm_tn(ctx, b, TC_SYRK))) break;
+      rc = launch_potrf_dag(ctx, dA + kend + (size_t)kend * lda, n - kend, lda, nullptr, 0, 0,
+                            kend, s0);
+      if (rc > 0) rc = set_err(ctx, GPR_E_HIP, "tile-DAG tail: shape not eligible");
+      tail_done = true;
+      break;
+    }
     // ---- square inverse of panel s, then (srhs mode) outer block s of B
     hipEvent_t ev_sq = sq_inverse(k, ev_p);
     if (!ev_sq) { rc = GPR_E_HIP; break; }
@@ -1803,6 +1826,8 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   int hinfo = 0;
   HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost, user));
   HIP_TRY(ctx, hipStreamSynchronize(user));
+  if (tail_done && hinfo < 0)
+    return set_err(ctx, GPR_E_HIP, "tile-DAG factorisation: a dependency wait timed out");
   if (info) *info = hinfo;
   if (hinfo == 0 && (sqp || rhs)) {
     ctx->sqinv_nb2 = nb2;

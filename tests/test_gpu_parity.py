@@ -265,6 +265,43 @@ def test_potrf_dag(n, monkeypatch):
     assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
 
 
+@pytest.mark.parametrize("n,nb2,tail", [(3008, 256, 1024), (2064, 512, 1600), (1040, 256, 1040),
+                                         (4096, 1024, 2048)])
+def test_potrf_dag_tail(n, nb2, tail, monkeypatch):
+    """Blocked factorisation that hands its last <= tail columns to the tile-DAG (GPR_DAG_TAIL):
+    one SYRK applies the last blocked panel to the whole trailing matrix, then the DAG factors
+    it with global block indices (solves read its W_i slots)."""
+    monkeypatch.setenv("GPR_DAG", "0")
+    monkeypatch.setenv("GPR_DAG_TAIL", str(tail))
+    ctx = G.Context(0)
+    assert G._lib.lib.gpr_set_outer_block(ctx.h, nb2) == 0
+    A = _spd(n, seed=n + nb2)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    R = ctx.host(dA)
+    U = sla.cholesky(A, lower=False)
+    assert relnorm(np.triu(R), U) < 1e-12
+    assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
+    B = np.random.default_rng(5).random((n, 3))
+    dB = ctx.colmajor(B)
+    assert G._lib.lib.gpr_potrs_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                      ctypes.c_void_p(dB.data_ptr()), 3, n) == 0
+    assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
+
+
+@pytest.mark.parametrize("j", [3, 300, 2000, 2999])
+def test_potrf_dag_tail_not_posdef_info(j, monkeypatch):
+    monkeypatch.setenv("GPR_DAG", "0")
+    monkeypatch.setenv("GPR_DAG_TAIL", "1024")
+    ctx = G.Context(0)
+    assert G._lib.lib.gpr_set_outer_block(ctx.h, 256) == 0
+    A = _spd(3008, seed=3)
+    A[j, j] = -1.0
+    _, info = _dev_potrf(ctx, A)
+    _, info_ref = sla.lapack.dpotrf(A, lower=0)
+    assert info == info_ref == j + 1
+
+
 @pytest.mark.parametrize("j", [0, 5, 127, 128, 200, 1000, 1039])
 def test_potrf_dag_not_posdef_info(j, monkeypatch):
     monkeypatch.setenv("GPR_DAG", "1")
@@ -692,6 +729,36 @@ def test_fit_predict_fused_vs_oracle(name, n, npred, dim, nb2, fused, monkeypatc
         _, S_o = O.predict(kinds, hp, x, y, xp, diagonal_var=False)
         np.testing.assert_allclose(mu2.ravel(), mu_o, rtol=1e-8, atol=1e-10)
         np.testing.assert_allclose(S, S_o, rtol=1e-8, atol=vtol)
+
+
+@pytest.mark.parametrize("name,n,npred,dim", [("SE+WN", 1040, 200, 3), ("SE+SE+WN", 2048, 300, 8),
+                                               ("SE+WN", 4112, 130, 4), ("SE", 256, 77, 8)])
+def test_fit_predict_dag_vs_oracle(name, n, npred, dim, monkeypatch):
+    """gpr_fit_predict with the tile-DAG (GPR_DAG=1): V = U^{-T} [K(x, xp) | y] solved by
+    right-hand-side tile tasks of the same persistent launch as the factorisation."""
+    monkeypatch.setenv("GPR_FUSED_RHS", "2")
+    monkeypatch.setenv("GPR_DAG", "1")
+    kinds = KSETS[name]
+    x, y, xp = O.synthetic(dim, n, npred, seed_train=n, seed_test=npred)
+    hp = O.default_hp(kinds, dim, noise=0.05)
+    ctx = G.Context(0)
+    Kd, alpha, mu, var = _fit_predict_dev(ctx, kinds, hp, x, y, xp, G.GPR_PREDICT_DIAG, None)
+    K = O.kernel(kinds, hp, x)
+    U = sla.cholesky(K, lower=False)
+    np.testing.assert_allclose(np.tril(Kd, -1), np.tril(K, -1), rtol=1e-13, atol=1e-15)
+    Kdev = np.tril(Kd) + np.tril(Kd, -1).T
+    np.fill_diagonal(Kdev, np.diag(K))
+    assert relnorm(np.triu(Kd), sla.cholesky(Kdev, lower=False)) < 1e-11
+    np.testing.assert_allclose(alpha.ravel(), O.cho_solve_upper(U, y), rtol=1e-8,
+                               atol=1e-10 * np.abs(O.cho_solve_upper(U, y)).max())
+    mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+    vtol = 1e-8 * O.diag_prior(kinds, hp, dim)
+    np.testing.assert_allclose(mu.ravel(), mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=vtol)
+    _, _, mu2, S = _fit_predict_dev(ctx, kinds, hp, x, y, xp, G.GPR_PREDICT_FULL, None)
+    _, S_o = O.predict(kinds, hp, x, y, xp, diagonal_var=False)
+    np.testing.assert_allclose(mu2.ravel(), mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(S, S_o, rtol=1e-8, atol=vtol)
 
 
 def test_fit_predict_multi_output_and_reuse():

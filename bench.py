@@ -7,9 +7,11 @@ reference has no periodic kernel), N = 32768 training points, d = 8, f
 One step = one GP job on each GPU, the reference's predict(md, xp; diagonal_var=true) from
 scratch (src/predict.jl:14-71: update_cache! = K, cholesky!, ldiv! against y; then predict!)
 as ONE call, gpr_fit_predict:
-    fit      : K-assembly (N x N) + in-place blocked POTRF + POTRS (alpha = K^{-1} y)
-    posterior: cross kernel (N x np) + mean + diagonal variance for np = 8192 test points
-(GPR_FUSED_RHS=1/2 solves [K(x, xp) | y] inside the factorisation instead: measured slower.)
+    K-assembly (N x N) and cross kernel K(x, xp) (N x np, np = 8192 test points); ONE
+    persistent tile-DAG launch factors K in place (upper Cholesky) and solves
+    U^T [V | z] = [K(x, xp) | y] as right-hand-side tile tasks; mean = V^T z, diagonal
+    variance = prior - ||V_j||^2, alpha = U^{-1} z (backward sweep).
+(GPR_DAG=0: the blocked two-stream factorisation, then POTRS and the posterior TRSM.)
 Synthetic data: x ~ U[0,1)^(d x N) seed 0 (+rank), y = sin(sum x)^2, test points
 seed 1 (+rank); hp sigma = 1, l = 3 sqrt(8/d), sigma_n = 0.1.  All inputs are resident in
 HBM before the timed region.
@@ -18,10 +20,12 @@ Multi-GPU: the fit does not shard (no distributed Cholesky) -- every 
 own job ("replicas", weak scaling, no data-path collective); value = jobs/s over all ranks.
 
 Extra fields: K-build GB/s (8 N^2 / t) and POTRF TFLOP/s ((N^3/3) / t) at N = 32768, stage
-times, and `roofline` for the dominant kernel (gemm_tn_kernel, the FP64 MFMA GEMM that runs
-every POTRF trailing update / panel and the posterior TRSM) measured with HIP events on the
-context stream over one instrumented step; `cpu_baseline` = the CPU oracle (threaded C
-K-build + OpenBLAS LAPACK) on a bounded sample (N = 8192, np = 2048), scaled to the job.
+times, and `roofline` for the dominant kernel -- potrf_dag_kernel, the persistent tile-DAG
+launch that factors K and solves U^T [V | z] = [K(x, xp) | y] (N^3/3 + N^2 (np + 1) flops),
+or, with GPR_DAG=0, the pipelined FP64 MFMA GEMM of the blocked path -- measured with HIP
+events on the stream it runs on over one instrumented step; `cpu_baseline` = the CPU oracle
+(threaded C K-build + OpenBLAS LAPACK) on a bounded sample (N = 8192, np = 2048), scaled to
+the job.
 """
 from __future__ import annotations
 
@@ -46,10 +50,12 @@ FP64_MFMA_PEAK = 78.6      # TFLOP/s, FP64 matrix spec (measured 77.7 in tools/p
 # the pipelined FP64 GEMM: two compiled variants of one kernel (beta != 0 preloads C, `z`
 # starts from zero); timing class 5 counts every launch of both
 DOMINANT_KERNELS = ("gemm_tn_pipe8_kernel", "gemm_tn_pipe8z_kernel")
+# the one-launch tile-DAG factorisation + posterior solve (dag.hip), the default since round 2
+DAG_KERNEL = "potrf_dag_kernel"
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 
 
-def pmc_traffic(kernels, n, npred):
+def pmc_traffic(kernels, n, npred, largest=False):
     """HBM bytes per launch (dispatch-weighted over `kernels`) from the newest committed PMC summary
     (profiles/rNN_pmc_summary.json, written by tools/profile_round.sh from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command, FETCH_SIZE
@@ -68,6 +74,10 @@ def pmc_traffic(kernels, n, npred):
             continue
         ks = [js.get("kernels", {}).get(k) for k in kernels]
         if not all(ks):
+            continue
+        if largest:  # the job's launch of a kernel also launched with less work per call
+            if all("traffic_bytes_max_launch" in k for k in ks):
+                return max(k["traffic_bytes_max_launch"] for k in ks)
             continue
         w = [k.get("trace", {}).get("calls") or k.get("dispatches_fetch_pass") or 1 for k in ks]
         return sum(wi * k["traffic_bytes_per_launch"] for wi, k in zip(w, ks)) / sum(w)
@@ -262,11 +272,19 @@ def main():
     kb_ms = cls["kbuild"][0]
     kbuild_gbs = 8.0 * N * N / (kb_ms * 1e-3) / 1e9
     potrf_tf = (N ** 3 / 3.0) / (stg["potrf"] * 1e-3) / 1e12
-    # dominant kernel: gemm_tn_pipe8_kernel (POTRF trailing SYRK, TRSM trailing updates),
-    # timed per launch with HIP events on the stream it is launched on (timing class 5)
-    g_ms, g_launch, g_fl = cls["gemm_pipe"]
+    # dominant kernel: the persistent tile-DAG launch (factorisation + the posterior solve of
+    # [K(x, xp) | y], timing class 6) when it ran, else the pipelined GEMM of the blocked path
+    # (timing class 5); each timed per launch with HIP events on the stream it runs on
+    if cls["dag"][1] > 0:
+        dominant = (DAG_KERNEL,)
+        g_ms, g_launch, g_fl = cls["dag"]
+    else:
+        dominant = DOMINANT_KERNELS
+        g_ms, g_launch, g_fl = cls["gemm_pipe"]
     achieved = g_fl / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
-    traffic = pmc_traffic(DOMINANT_KERNELS, N, NP)
+    # the DAG kernel also runs alone (factorisation only) in the stage breakdown: its traffic
+    # per JOB launch is the largest of the profiled launches
+    traffic = pmc_traffic(dominant, N, NP, largest=dominant == (DAG_KERNEL,))
 
     out = None
     if rank == 0:
@@ -298,7 +316,7 @@ def main():
             "dag_ms": cls["dag"][0], "dag_launches": cls["dag"][1],
             "dag_TFLOPs": cls["dag"][2] / (cls["dag"][0] * 1e-3) / 1e12 if cls["dag"][0] else None,
             "roofline": {
-                "kernel": " + ".join(DOMINANT_KERNELS),
+                "kernel": " + ".join(dominant),
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": FP64_MFMA_PEAK,

@@ -65,19 +65,19 @@ struct gpr_ctx {
                                   // fused_rhs_nmax), 0 off, 1/2 forced (GPR_FUSED_RHS)
   int fused_rhs_nmax = 16384;     // GPR_FUSED_RHS_NMAX
   int fuse_y = 0;
-  int fuse_kinv = 2;              // gpr_fit_kinv: Z = U^{-T} solved inside the factorisation
+  int fuse_kinv = -1;             // gpr_fit_kinv (-1 auto: 0 when the tile-DAG factors, else 2):
+                                  // Z = U^{-T} solved inside the blocked factorisation
                                   // (1), and K^{-1} = Z^T Z accumulated there too (2)                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   // persistent tile-DAG factorisation (dag.hip): 0 off, 1 on for dag_nmin <= n <= dag_nmax
   // (GPR_DAG, GPR_DAG_NMIN, GPR_DAG_NMAX); the task list is cached per (tiles, rhs tiles).
-  // Measured (POTRF alone): N = 8192 9.3 -> 6.9 ms, 16384 34.5 -> 29.6; at 32768 the DAG's
-  // tile tasks (53 TF/s) lose to the blocked trailing SYRKs (61), so larger factorisations
-  // keep the blocked path and hand only their chain-bound tail to the DAG.
+  // Measured (POTRF alone, blocked -> DAG): N = 8192 9.3 -> 6.8 ms, 16384 34.5 -> 25.0,
+  // 32768 193 -> 173.4 (67.7 TF/s); C3 fit + predict in one DAG launch 321.8 -> 305.5 ms.
   int dag_mode = 1;
-  int dag_nmin = 0, dag_nmax = 16384;
-  int dag_tail = 12288;  // blocked factorisations hand their last <= dag_tail columns to the
-                         // DAG (GPR_DAG_TAIL; 0 = off): C3 POTRF 193.5 -> 188.3 ms
+  int dag_nmin = 0, dag_nmax = 1 << 30;
+  int dag_tail = 12288;  // blocked factorisations (GPR_DAG=0, ineligible sizes) hand their last
+                         // <= dag_tail columns to the DAG (GPR_DAG_TAIL; 0 = off)
   unsigned* dag_tasks = nullptr;
   int dag_ntasks = 0, dag_nt = -1, dag_ntr = -1;
   int* dag_sync = nullptr;
@@ -224,6 +224,8 @@ struct RhsSpec {
 // one-launch tile-DAG factorisation (+ B <- U^{-T} B); 1 = shape not eligible, 0 = launched
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
                      int kglob, hipStream_t st);
+// true when potrf_core would factor (n, lda, dA) as ONE tile-DAG launch
+bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA);
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
                const RhsSpec* rhs = nullptr);
 int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);

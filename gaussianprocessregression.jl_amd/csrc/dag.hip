@@ -261,8 +261,14 @@ __device__ __attribute__((noinline)) int dag_factor(double* S, double* T, size_t
 }
 
 __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
-  __shared__ double lds[DLDS];
-  __shared__ int s_task, s_skip, s_wait;
+  // ONE LDS variable: with separate __shared__ scalars the accesses get alias scopes, and
+  // the waitcnt pass then made every fragment read wait for ALL in-flight LDS-DMA (an
+  // s_waitcnt vmcnt(0) per stage: the DMA never ran ahead; accumulation at 0.23 instead of
+  // ~0.28 TF/s per CU)
+  __shared__ double lds[DLDS + 2];
+  int& s_task = reinterpret_cast<int*>(lds + DLDS)[0];
+  int& s_skip = reinterpret_cast<int*>(lds + DLDS)[1];
+  int& s_wait = reinterpret_cast<int*>(lds + DLDS)[2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w & 1, wn = w >> 1;
@@ -406,6 +412,11 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
 // Factor A (n x n, ld lda) in place and, when B != nullptr, B <- U^{-T} B (n x nrhs, ld ldb),
 // in one launch on ctx->stream.  Writes W_i into ctx->winv slots (block inverses for the
 // solves).  Returns 1 when the shape does not qualify (caller falls back), 0 when launched.
+bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA) {
+  return ctx->dag_mode && n >= ctx->dag_nmin && n <= ctx->dag_nmax && ctx->nb == DT && n > 0 &&
+         n % 16 == 0 && lda % 16 == 0 && ((uintptr_t)dA & 127) == 0 && n <= DT * 32767;
+}
+
 // kglob: global index of A's first row/column (the trailing matrix of a blocked factorisation:
 // block inverses go to winv slots kglob/128 + i, pivot orders are global); st: the stream.
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,

@@ -270,17 +270,20 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   // solved, so the N^3/3-flop Gram product fills the chain-bound half of the factorisation
   // instead of running after it
   RhsSpec rhs{Z, n, n, 1, ctx->fused_rhs == 2 ? 2 : 1, nullptr, 0};
-  if (ctx->fuse_kinv == 2) {
+  // auto (-1): when the tile-DAG takes the factorisation, factor first (one DAG launch), then
+  // Z and Z^T Z; the fused forms below ride the blocked factorisation's lookahead bubbles
+  const int fuse = ctx->fuse_kinv >= 0 ? ctx->fuse_kinv : (dag_takes_whole(ctx, n, ldk, dK) ? 0 : 2);
+  if (fuse == 2) {
     HIP_TRY(ctx, hipMemset2DAsync(dKinv, (size_t)ldkinv * sizeof(double), 0,
                                   (size_t)n * sizeof(double), n, ctx->stream));
     rhs.gram = dKinv;
     rhs.ldg = ldkinv;
   }
-  GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, ctx->fuse_kinv ? &rhs : nullptr));
+  GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, fuse ? &rhs : nullptr));
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
   GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
-  if (!ctx->fuse_kinv) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
+  if (!fuse) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
   if (rhs.gram) return launch_mirror_upper(ctx, dKinv, n, ldkinv);
   return kinv_from_z(ctx, Z, n, dKinv, ldkinv);
 }
@@ -299,7 +302,11 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   // chain-bound and leaves the GPU idle: measured C2 (n = 8192, np = 8192) 21.0 -> 18.9 ms,
   // n = 16384 70.9 -> 67.3; at n = 32768 the trailing SYRKs fill the GPU and the fused
   // solve slows them (r01: 347 vs 334 ms), so auto fuses only up to fused_rhs_nmax.
-  const int fmode = ctx->fused_rhs < 0 ? (n <= ctx->fused_rhs_nmax ? 2 : 0) : ctx->fused_rhs;
+  // When the tile-DAG takes the whole factorisation, [K(x, xp) | y] rides in it as right-hand-
+  // side tile tasks (the same launch), so auto fuses whenever the DAG applies.
+  const int fmode = ctx->fused_rhs < 0
+                        ? ((n <= ctx->fused_rhs_nmax || dag_takes_whole(ctx, n, ldk, dK)) ? 2 : 0)
+                        : ctx->fused_rhs;
   if (mode == GPR_PREDICT_MEAN || !fmode) {
     // nothing to fuse for the mean alone (mu = K(xp, x) alpha); or the unfused reference order
     double* wt = dalpha;

@@ -32,6 +32,16 @@ def per_dispatch(pattern, counter):
     return {k: tot[k] / max(len(cnt[k]), 1) for k in tot}, {k: len(v) for k, v in cnt.items()}
 
 
+def per_dispatch_list(pattern, counter):
+    """{kernel: [counter sum of each dispatch, in dispatch order]}"""
+    vals = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(pattern, recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                vals[short(r["Kernel_Name"])][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+    return {k: [v[i] for i in sorted(v)] for k, v in vals.items()}
+
+
 def trace_stats(pattern):
     out = {}
     for f in glob.glob(pattern, recursive=True):
@@ -47,6 +57,11 @@ def main():
     fetch, nf = per_dispatch(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
     write, nw = per_dispatch(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
     stats = trace_stats(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
+    # per-dispatch traffic, the two passes paired by dispatch order (same command): a kernel
+    # launched with different work per call (the tile-DAG: fit + posterior solve in the job,
+    # factorisation alone in the stage breakdown) is characterised by its largest launch too
+    fl = per_dispatch_list(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
+    wl = per_dispatch_list(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         fb = 2.0 * fetch.get(k, 0.0) * 1024.0
@@ -54,6 +69,11 @@ def main():
         kernels[k] = {"dispatches_fetch_pass": nf.get(k, 0), "dispatches_write_pass": nw.get(k, 0),
                       "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                       "traffic_bytes_per_launch": fb + wb, "trace": stats.get(k)}
+        f1, w1 = fl.get(k, []), wl.get(k, [])
+        if f1 and len(f1) == len(w1):
+            per = [2.0 * a * 1024.0 + b * 1024.0 for a, b in zip(f1, w1)]
+            kernels[k]["traffic_bytes_each_launch"] = per
+            kernels[k]["traffic_bytes_max_launch"] = max(per)
     out = {"config": {"N": n, "np": npred},
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
                      "`bench.py --steps 1 --warmup 0 --no-cpu-baseline`; FETCH_SIZE x2 (gfx950 "

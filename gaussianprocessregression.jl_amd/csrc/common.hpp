@@ -76,10 +76,11 @@ struct gpr_ctx {
   // 32768 193 -> 173.4 (67.7 TF/s); C3 fit + predict in one DAG launch 321.8 -> 305.5 ms.
   int dag_mode = 1;
   int dag_nmin = 0, dag_nmax = 1 << 30;
+  int dag_solve = 0;      // solves from a finished factor as solve-only DAG launches (GPR_DAG_SOLVE)
   int dag_tail = 12288;  // blocked factorisations (GPR_DAG=0, ineligible sizes) hand their last
                          // <= dag_tail columns to the DAG (GPR_DAG_TAIL; 0 = off)
   unsigned* dag_tasks = nullptr;
-  int dag_ntasks = 0, dag_nt = -1, dag_ntr = -1;
+  int dag_ntasks = 0, dag_nt = -1, dag_ntr = -1, dag_flags = -1;
   int* dag_sync = nullptr;
   size_t dag_sync_cap = 0;
   int ncu = 0;
@@ -222,8 +223,9 @@ struct RhsSpec {
   int ldg;
 };
 // one-launch tile-DAG factorisation (+ B <- U^{-T} B); 1 = shape not eligible, 0 = launched
+enum { DAG_SOLVE = 1, DAG_LOWER = 2 };
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
-                     int kglob, hipStream_t st);
+                     int kglob, hipStream_t st, int flags = 0);
 // true when potrf_core would factor (n, lda, dA) as ONE tile-DAG launch
 bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA);
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,

@@ -97,6 +97,8 @@ struct DagArgs {
   int* sync;     // [0] ticket, [2 + j] colprog[j], [2 + nt + c] rhsprog[c]
   const unsigned* tasks;
   int ntasks;
+  int lower;     // B is lower triangular (the identity's solve Z = U^{-T}): tile (i, c) exists
+                 // for i >= c only and accumulates row blocks [c, i)
 };
 
 __device__ __forceinline__ int ld_sc1(const int* p) {
@@ -325,7 +327,7 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
         }
       // acc += sum_{k<i} U_ki^T X_kj, row blocks taken as soon as both columns have them final
       DTRACE(1, 2);
-      int done = 0;
+      int done = (rhs && a.lower) ? j : 0;
       while (done < i) {
         int r = 0;
         PROF(p_wait, r = dag_wait(colprog + i, pj, done, i, a.info, &s_wait));
@@ -409,30 +411,44 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
 
 }  // namespace
 
-// Factor A (n x n, ld lda) in place and, when B != nullptr, B <- U^{-T} B (n x nrhs, ld ldb),
-// in one launch on ctx->stream.  Writes W_i into ctx->winv slots (block inverses for the
-// solves).  Returns 1 when the shape does not qualify (caller falls back), 0 when launched.
+// Progress counters of a launch that starts from a finished factor (DAG_SOLVE: every tile of
+// U final, colprog[j] = j + 1) and/or a lower-triangular B (DAG_LOWER: tiles (k < c, c) of B
+// are the identity's zeros, final from the start: rhsprog[c] = c).
+__global__ void dag_init_kernel(int* sync, int nt, int ntr, int solve, int lower) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt + ntr; t += gridDim.x * blockDim.x)
+    sync[2 + t] = t < nt ? (solve ? t + 1 : 0) : (lower ? t - nt : 0);
+}
+
 bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA) {
   return ctx->dag_mode && n >= ctx->dag_nmin && n <= ctx->dag_nmax && ctx->nb == DT && n > 0 &&
          n % 16 == 0 && lda % 16 == 0 && ((uintptr_t)dA & 127) == 0 && n <= DT * 32767;
 }
 
+// Factor A (n x n, ld lda) in place and, when B != nullptr, B <- U^{-T} B (n x nrhs, ld ldb),
+// in one launch on st.  Writes W_i into ctx->winv slots (block inverses for the solves).
 // kglob: global index of A's first row/column (the trailing matrix of a blocked factorisation:
-// block inverses go to winv slots kglob/128 + i, pivot orders are global); st: the stream.
+// block inverses go to winv slots kglob/128 + i, pivot orders are global).  flags: DAG_SOLVE
+// (A already holds U and winv its block inverses: only B's tiles are tasks), DAG_LOWER (B is
+// lower triangular, e.g. the identity).  Returns 1 when the shape does not qualify (caller
+// falls back), 0 when launched.
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
-                     int kglob, hipStream_t st) {
+                     int kglob, hipStream_t st, int flags) {
+  const bool solve = flags & DAG_SOLVE, lower = flags & DAG_LOWER;
+  if ((solve || lower) && (!dB || kglob)) return 1;
   if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || ((uintptr_t)dA & 127) || n > DT * 32767 ||
       kglob % DT)
     return 1;
   if (dB && (nrhs <= 0 || ldb % 16 || ((uintptr_t)dB & 127) || nrhs > DT * 65535)) return 1;
   const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
   GPR_TRY(ensure_winv(ctx, kglob + n, DT));
-  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr) {
+  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != flags) {
     std::vector<unsigned> tasks;
     tasks.reserve((size_t)nt * (nt + 1) / 2 + (size_t)nt * ntr);
     for (int i = 0; i < nt; ++i) {
-      for (int j = i; j < nt; ++j) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
-      for (int c = 0; c < ntr; ++c) tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
+      if (!solve)
+        for (int j = i; j < nt; ++j) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
+      for (int c = 0; c < (lower ? std::min(ntr, i + 1) : ntr); ++c)
+        tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
     }
     if (ctx->dag_tasks) hipFree(ctx->dag_tasks);
     ctx->dag_tasks = nullptr;
@@ -443,6 +459,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_ntasks = (int)tasks.size();
     ctx->dag_nt = nt;
     ctx->dag_ntr = ntr;
+    ctx->dag_flags = flags;
   }
   const size_t nsync = 2 + (size_t)nt + ntr;
   if (ctx->dag_sync_cap < nsync) {
@@ -453,6 +470,10 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_sync_cap = nsync;
   }
   HIP_TRY(ctx, hipMemsetAsync(ctx->dag_sync, 0, nsync * sizeof(int), st));
+  if (solve || lower) {
+    dag_init_kernel<<<(nt + ntr + 255) / 256, 256, 0, st>>>(ctx->dag_sync, nt, ntr, solve, lower);
+    LAUNCH_CHECK(ctx);
+  }
   if (ctx->ncu <= 0) {
     hipDeviceProp_t prop;
     HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
@@ -473,8 +494,11 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   a.sync = ctx->dag_sync;
   a.tasks = ctx->dag_tasks;
   a.ntasks = ctx->dag_ntasks;
+  a.lower = lower;
   const int grid = std::min(ctx->dag_ntasks, ctx->ncu);
-  const double flops = (double)n * n * n / 3.0 + (double)n * n * (dB ? nrhs : 0);
+  // factorisation n^3/3; U^{-T} B: n^2 per column, ~n^3/3 for a lower-triangular n x n B
+  const double flops = (solve ? 0.0 : (double)n * n * n / 3.0) +
+                       (lower ? (double)n * n * n / 3.0 : (double)n * n * (dB ? nrhs : 0));
   {
     hipStream_t ls = ctx->ls;
     ctx->ls = st;  // TimerScope records on ctx->ls

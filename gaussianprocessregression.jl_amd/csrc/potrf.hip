@@ -1639,11 +1639,12 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     GPR_TRY(ensure_buf(ctx, &ctx->dpanel_rhs, &ctx->panel_rhs_cap, (size_t)nb2 * rhs->nrhs));
   }
   if (ctx->dag_mode && n >= ctx->dag_nmin && n <= ctx->dag_nmax &&
-      (!rhs || (!rhs->gram && !rhs->lower_rhs))) {
+      (!rhs || (!rhs->gram && (!rhs->lower_rhs || rhs->nrhs == n)))) {
     // one persistent launch: tiles handed between workgroups by progress counters
     HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
     const int rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
-                                    rhs ? rhs->ldb : 0, 0, ctx->stream);
+                                    rhs ? rhs->ldb : 0, 0, ctx->stream,
+                                    rhs && rhs->lower_rhs ? DAG_LOWER : 0);
     if (rc < 0) return rc;
     if (rc == 0) {
       int hinfo = 0;
@@ -1945,6 +1946,19 @@ int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols
 
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs) {
+  if (ctx->dag_solve && dag_takes_whole(ctx, n, ldu, dU) && nrhs >= 128 &&
+      (!lower_rhs || nrhs == n)) {
+    // the tile-DAG with every tile of U final: only B's tiles are tasks (left-looking, one
+    // long-K accumulation per tile, W_i from the factor's block inverses)
+    GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
+    const int rc = launch_potrf_dag(ctx, const_cast<double*>(dU), n, ldu, dB, nrhs, ldb, 0,
+                                    ctx->stream, DAG_SOLVE | (lower_rhs ? DAG_LOWER : 0));
+    if (rc < 0) return rc;
+    if (rc == 0) {
+      if (norm_out) GPR_TRY(launch_colnorm_sub(ctx, dB, ldb, n, nrhs, norm_out));
+      return 0;
+    }
+  }
   {
     const int sqok = ensure_sq_inverses(ctx, dU, n, ldu);
     if (sqok < 0) return sqok;

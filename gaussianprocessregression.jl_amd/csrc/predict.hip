@@ -270,8 +270,9 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   // solved, so the N^3/3-flop Gram product fills the chain-bound half of the factorisation
   // instead of running after it
   RhsSpec rhs{Z, n, n, 1, ctx->fused_rhs == 2 ? 2 : 1, nullptr, 0};
-  // auto (-1): when the tile-DAG takes the factorisation, factor first (one DAG launch), then
-  // Z and Z^T Z; the fused forms below ride the blocked factorisation's lookahead bubbles
+  // auto (-1): when the tile-DAG takes the factorisation, factor (one DAG launch), then Z and
+  // Z^T Z (0; Z as lower-triangular right-hand-side tasks of the DAG launch, 1, measured
+  // slower); otherwise (2) both ride the blocked factorisation's lookahead bubbles
   const int fuse = ctx->fuse_kinv >= 0 ? ctx->fuse_kinv : (dag_takes_whole(ctx, n, ldk, dK) ? 0 : 2);
   if (fuse == 2) {
     HIP_TRY(ctx, hipMemset2DAsync(dKinv, (size_t)ldkinv * sizeof(double), 0,

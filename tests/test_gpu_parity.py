@@ -407,8 +407,12 @@ def test_potrs_sweeps_under_uneven_load():
     side.synchronize()
 
 
-@pytest.mark.parametrize("n", [100, 300, 513])
-def test_potri_and_trsm(n):
+@pytest.mark.parametrize("n", [100, 300, 513, 256, 1040])
+@pytest.mark.parametrize("dag_solve", ["0", "1"])
+def test_potri_and_trsm(n, dag_solve, monkeypatch):
+    """K^{-1} and B <- U^{-T} B from a factor; dag_solve=1: the solve-only tile-DAG (every
+    tile of U final, only B's tiles are tasks; lower-triangular B for K^{-1}'s Z = U^{-T})."""
+    monkeypatch.setenv("GPR_DAG_SOLVE", dag_solve)
     ctx = G.Context(0)
     A = _spd(n, seed=9)
     dA, info = _dev_potrf(ctx, A)
@@ -419,14 +423,15 @@ def test_potri_and_trsm(n):
     Kinv = ctx.host(dK)
     assert relnorm(Kinv, np.linalg.inv(A)) < 1e-11
     assert np.array_equal(Kinv, Kinv.T)
-    # trsm: B <- U^{-T} B
-    B = np.random.default_rng(2).random((n, 37))
-    dB = ctx.colmajor(B)
-    rc = G._lib.lib.gpr_trsm_upper_trans(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
-                                        ctypes.c_void_p(dB.data_ptr()), 37, n)
-    assert rc == 0
+    # trsm: B <- U^{-T} B (>= 128 columns at n % 16 == 0: the solve-only tile-DAG)
     U = sla.cholesky(A, lower=False)
-    assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11
+    for nr in (37, 300):
+        B = np.random.default_rng(2).random((n, nr))
+        dB = ctx.colmajor(B)
+        rc = G._lib.lib.gpr_trsm_upper_trans(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
+                                            ctypes.c_void_p(dB.data_ptr()), nr, n)
+        assert rc == 0
+        assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11
 
 
 # ---------------------------------------------------------------------------------------
@@ -518,7 +523,8 @@ def test_log_loss_grad_and_composed():
 # a10/a11 posterior  (test/test_models.jl)
 # ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("name", ["SE", "SE+WN", "SE+SE", "SE+SE+WN"])
-@pytest.mark.parametrize("n,npred,dim", [(100, 100, 1), (200, 500, 2), (500, 200, 5), (333, 77, 8)])
+@pytest.mark.parametrize("n,npred,dim", [(100, 100, 1), (200, 500, 2), (500, 200, 5), (333, 77, 8),
+                                         (1024, 300, 4)])
 def test_predict_vs_oracle(name, n, npred, dim):
     kinds = KSETS[name]
     x, y, xp = O.synthetic(dim, n, npred, seed_train=n, seed_test=npred)
@@ -789,7 +795,8 @@ def test_fit_predict_multi_output_and_reuse():
 
 
 @pytest.mark.parametrize("fuse", ["2", "1", "0"])
-@pytest.mark.parametrize("n,nb2", [(300, None), (1300, 256), (2100, 1024), (777, 512)])
+@pytest.mark.parametrize("n,nb2", [(300, None), (1300, 256), (2100, 1024), (777, 512), (1040, None),
+                                   (2048, None)])
 def test_fit_kinv(n, nb2, fuse, monkeypatch):
     """gpr_fit_kinv = update_cache!(::MllGradCache) (src/cost.jl:83-111): U, alpha and the
     dense K^{-1}, with Z = U^{-T} solved inside the factorisation and K^{-1} = Z^T Z

@@ -450,7 +450,12 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
       for (int c = 0; c < (lower ? std::min(ntr, i + 1) : ntr); ++c)
         tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
     }
-    if (ctx->dag_tasks) hipFree(ctx->dag_tasks);
+    // a previous launch on this context may still be reading the old list (solves do not
+    // synchronise): drain the context's stream before freeing it
+    if (ctx->dag_tasks) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (every DAG launch joins it)
+      HIP_TRY(ctx, hipFree(ctx->dag_tasks));
+    }
     ctx->dag_tasks = nullptr;
     ctx->dag_nt = ctx->dag_ntr = -1;
     HIP_TRY(ctx, hipMalloc((void**)&ctx->dag_tasks, tasks.size() * sizeof(unsigned)));
@@ -463,7 +468,10 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   }
   const size_t nsync = 2 + (size_t)nt + ntr;
   if (ctx->dag_sync_cap < nsync) {
-    if (ctx->dag_sync) hipFree(ctx->dag_sync);
+    if (ctx->dag_sync) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (every DAG launch joins it)
+      HIP_TRY(ctx, hipFree(ctx->dag_sync));
+    }
     ctx->dag_sync = nullptr;
     ctx->dag_sync_cap = 0;
     HIP_TRY(ctx, hipMalloc((void**)&ctx->dag_sync, nsync * sizeof(int)));

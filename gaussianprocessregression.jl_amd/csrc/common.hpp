@@ -83,6 +83,10 @@ struct gpr_ctx {
   int dag_ntasks = 0, dag_nt = -1, dag_ntr = -1, dag_flags = -1;
   int* dag_sync = nullptr;
   size_t dag_sync_cap = 0;
+  double* dpadA = nullptr;  // padded copies for shapes the DAG launch does not take directly
+  size_t padA_cap = 0;
+  double* dpadB = nullptr;
+  size_t padB_cap = 0;
   int ncu = 0;
   std::vector<hipEvent_t> sync_events;
   size_t ev_next = 0;
@@ -226,8 +230,12 @@ struct RhsSpec {
 enum { DAG_SOLVE = 1, DAG_LOWER = 2 };
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
                      int kglob, hipStream_t st, int flags = 0);
-// true when potrf_core would factor (n, lda, dA) as ONE tile-DAG launch
+// true when potrf_core would factor (n, lda, dA) as ONE tile-DAG launch (directly, or for
+// other shapes on a padded copy); dag_shape_ok: the launch takes the shape directly
 bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA);
+bool dag_shape_ok(int n, int lda, const double* dA);
+int launch_potrf_dag_padded(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs,
+                            int ldb);
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,
                const RhsSpec* rhs = nullptr);
 int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);

@@ -419,9 +419,80 @@ __global__ void dag_init_kernel(int* sync, int nt, int ntr, int solve, int lower
     sync[2 + t] = t < nt ? (solve ? t + 1 : 0) : (lower ? t - nt : 0);
 }
 
+// The launch's own shape conditions: every 128-B line belongs to one tile (leading dimensions
+// multiples of 16 doubles, 128-B aligned bases) and every K range is a multiple of the 16-row
+// pipeline stage (n % 16 == 0).
+bool dag_shape_ok(int n, int lda, const double* dA) {
+  return n > 0 && n % 16 == 0 && lda % 16 == 0 && ((uintptr_t)dA & 127) == 0 && n <= DT * 32767;
+}
+
+// true when potrf_core factors (n, lda, dA) as one tile-DAG launch: directly, or for any other
+// shape through a padded copy (dag_padded)
 bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA) {
+  (void)lda;
+  (void)dA;
   return ctx->dag_mode && n >= ctx->dag_nmin && n <= ctx->dag_nmax && ctx->nb == DT && n > 0 &&
-         n % 16 == 0 && lda % 16 == 0 && ((uintptr_t)dA & 127) == 0 && n <= DT * 32767;
+         n <= DT * 32767 - 16;
+}
+
+// upper triangle of A (n x n, ld lda) into W (n2 x n2, ld n2), identity beyond n: the padded
+// matrix [[A, 0], [0, I]] has the factor [[U, 0], [0, I]] and the same block inverses on its
+// first n rows, and the tile-DAG's arithmetic on the first n rows is unchanged by the padding
+__global__ void dag_pad_in_kernel(const double* __restrict__ A, size_t lda, int n,
+                                  double* __restrict__ W, int n2) {
+  const size_t tot = (size_t)n2 * n2;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < tot;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t % n2), c = (int)(t / n2);
+    if (r <= c) W[t] = c < n ? A[(size_t)r + (size_t)c * lda] : (r == c ? 1.0 : 0.0);
+  }
+}
+
+// U (upper, first n rows / columns of W) back into A; A's strict lower triangle untouched
+__global__ void dag_pad_out_kernel(double* __restrict__ A, size_t lda, int n,
+                                   const double* __restrict__ W, int n2) {
+  const size_t tot = (size_t)n * n;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < tot;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t % n), c = (int)(t / n);
+    if (r <= c) A[(size_t)r + (size_t)c * lda] = W[(size_t)r + (size_t)c * n2];
+  }
+}
+
+// The factorisation (and B <- U^{-T} B) of a shape the launch does not take directly, on a
+// padded copy: n2 = n rounded up to 16, ld n2.  Costs one read + write of the upper triangle
+// each way (and of B); returns 1 when the workspace cannot be allocated (caller falls back).
+int launch_potrf_dag_padded(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs,
+                            int ldb) {
+  const int n2 = (n + 15) / 16 * 16;
+  hipStream_t st = ctx->stream;
+  if (ensure_buf(ctx, &ctx->dpadA, &ctx->padA_cap, (size_t)n2 * n2) != 0 ||
+      (dB && ensure_buf(ctx, &ctx->dpadB, &ctx->padB_cap, (size_t)n2 * nrhs) != 0)) {
+    ctx->err.clear();
+    (void)hipGetLastError();  // do not leave the allocation failure for the next launch check
+    return 1;
+  }
+  const int blocks = 2048;
+  dag_pad_in_kernel<<<blocks, 256, 0, st>>>(dA, (size_t)lda, n, ctx->dpadA, n2);
+  LAUNCH_CHECK(ctx);
+  if (dB) {
+    HIP_TRY(ctx, hipMemcpy2DAsync(ctx->dpadB, (size_t)n2 * sizeof(double), dB,
+                                  (size_t)ldb * sizeof(double), (size_t)n * sizeof(double), nrhs,
+                                  hipMemcpyDeviceToDevice, st));
+    if (n2 > n)
+      HIP_TRY(ctx, hipMemset2DAsync(ctx->dpadB + n, (size_t)n2 * sizeof(double), 0,
+                                    (size_t)(n2 - n) * sizeof(double), nrhs, st));
+  }
+  const int rc = launch_potrf_dag(ctx, ctx->dpadA, n2, n2, dB ? ctx->dpadB : nullptr, nrhs, n2, 0,
+                                  st, 0);
+  if (rc) return rc < 0 ? rc : set_err(ctx, GPR_E_HIP, "padded tile-DAG: shape not eligible");
+  dag_pad_out_kernel<<<blocks, 256, 0, st>>>(dA, (size_t)lda, n, ctx->dpadA, n2);
+  LAUNCH_CHECK(ctx);
+  if (dB)
+    HIP_TRY(ctx, hipMemcpy2DAsync(dB, (size_t)ldb * sizeof(double), ctx->dpadB,
+                                  (size_t)n2 * sizeof(double), (size_t)n * sizeof(double), nrhs,
+                                  hipMemcpyDeviceToDevice, st));
+  return 0;
 }
 
 // Factor A (n x n, ld lda) in place and, when B != nullptr, B <- U^{-T} B (n x nrhs, ld ldb),

@@ -240,6 +240,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->smain) hipStreamDestroy(ctx->smain);
   if (ctx->dag_tasks) hipFree(ctx->dag_tasks);
   if (ctx->dag_sync) hipFree(ctx->dag_sync);
+  if (ctx->dpadA) hipFree(ctx->dpadA);
+  if (ctx->dpadB) hipFree(ctx->dpadB);
   if (ctx->winv) hipFree(ctx->winv);
   if (ctx->dinfo) hipFree(ctx->dinfo);
   if (ctx->dexptab) hipFree(ctx->dexptab);

@@ -1638,13 +1638,19 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
                        (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));
     GPR_TRY(ensure_buf(ctx, &ctx->dpanel_rhs, &ctx->panel_rhs_cap, (size_t)nb2 * rhs->nrhs));
   }
-  if (ctx->dag_mode && n >= ctx->dag_nmin && n <= ctx->dag_nmax &&
+  if (dag_takes_whole(ctx, n, lda, dA) &&
       (!rhs || (!rhs->gram && (!rhs->lower_rhs || rhs->nrhs == n)))) {
-    // one persistent launch: tiles handed between workgroups by progress counters
+    // one persistent launch: tiles handed between workgroups by progress counters; shapes the
+    // launch does not take directly go through a padded copy
     HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
-    const int rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
-                                    rhs ? rhs->ldb : 0, 0, ctx->stream,
-                                    rhs && rhs->lower_rhs ? DAG_LOWER : 0);
+    int rc = 1;
+    if (dag_shape_ok(n, lda, dA))  // (1 = B's layout not taken directly either)
+      rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
+                            rhs ? rhs->ldb : 0, 0, ctx->stream,
+                            rhs && rhs->lower_rhs ? DAG_LOWER : 0);
+    if (rc == 1 && (!rhs || !rhs->lower_rhs))
+      rc = launch_potrf_dag_padded(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
+                                   rhs ? rhs->ldb : 0);
     if (rc < 0) return rc;
     if (rc == 0) {
       int hinfo = 0;

@@ -476,6 +476,10 @@ static int run_children(gpr_ctx* ctx, int nsub, const std::function<int(gpr_ctx*
       c->big_cap = 0;
       if (c->dbig2) hipFree(c->dbig2);  // fused fit+predict workspace of the folds
       c->dbig2 = nullptr;
+      if (c->dpadA) hipFree(c->dpadA);  // padded copies of odd-shaped folds
+      if (c->dpadB) hipFree(c->dpadB);
+      c->dpadA = c->dpadB = nullptr;
+      c->padA_cap = c->padB_cap = 0;
       c->big2_cap = 0;
       c->fac_valid = false;  // cached factor data were keyed on pointers into dbig
       c->sqinv_nb2 = 0;

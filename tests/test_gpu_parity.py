@@ -201,6 +201,8 @@ def _panel_env(monkeypatch, mode):
     """Panel schedule under test: "0" per-block full-width panel, "1" square-panel kernel,
     "la2" block lookahead, "ll" square chain + left-looking strip (GPR_PANEL=2), "inv" square
     chain + strip by the square's inverse (GPR_PANEL=3), "rec" recursive halves (GPR_PANEL=4)."""
+    monkeypatch.setenv("GPR_DAG", "0")  # the blocked factorisation's panel schedules
+    monkeypatch.setenv("GPR_DAG_TAIL", "0")
     monkeypatch.setenv("GPR_PANEL_SQ", mode if mode in ("0", "1") else "0")
     monkeypatch.setenv("GPR_INNER_LA", "2" if mode == "la2" else "0")
     monkeypatch.setenv("GPR_PANEL", {"ll": "2", "inv": "3", "rec": "4"}.get(mode, "0"))
@@ -244,11 +246,12 @@ def test_potrf_not_posdef_info_later_panels(j, panel_sq, monkeypatch):
     assert info == info_ref == j + 1
 
 
-@pytest.mark.parametrize("n", [16, 128, 144, 256, 400, 1040, 2064, 4112])
+@pytest.mark.parametrize("n", [16, 128, 144, 256, 400, 1040, 2064, 4112, 1, 50, 129, 333, 1031])
 def test_potrf_dag(n, monkeypatch):
     """Persistent tile-DAG factorisation (dag.hip, GPR_DAG=1): one launch, tiles handed
     between workgroups by progress counters; ragged last tile (n % 128 != 0), upper factor,
-    lower triangle untouched, block inverses usable by the solves."""
+    lower triangle untouched, block inverses usable by the solves.  n % 16 != 0 goes through
+    the padded copy [[A, 0], [0, I]]."""
     monkeypatch.setenv("GPR_DAG", "1")
     ctx = G.Context(0)
     A = _spd(n, seed=n + 7)
@@ -712,6 +715,9 @@ def test_fit_predict_fused_vs_oracle(name, n, npred, dim, nb2, fused, monkeypatc
     outer-panel boundaries (the solve rides inside the factorisation) and ragged panels;
     fused=0 is the unfused reference order (gpr_fit + gpr_predict)."""
     monkeypatch.setenv("GPR_FUSED_RHS", fused)
+    if fused != "0":  # the right-hand sides inside the BLOCKED factorisation
+        monkeypatch.setenv("GPR_DAG", "0")
+        monkeypatch.setenv("GPR_DAG_TAIL", "0")
     kinds = KSETS[name]
     x, y, xp = O.synthetic(dim, n, npred, seed_train=n, seed_test=npred)
     hp = O.default_hp(kinds, dim, noise=0.05)
@@ -738,7 +744,8 @@ def test_fit_predict_fused_vs_oracle(name, n, npred, dim, nb2, fused, monkeypatc
 
 
 @pytest.mark.parametrize("name,n,npred,dim", [("SE+WN", 1040, 200, 3), ("SE+SE+WN", 2048, 300, 8),
-                                               ("SE+WN", 4112, 130, 4), ("SE", 256, 77, 8)])
+                                               ("SE+WN", 4112, 130, 4), ("SE", 256, 77, 8),
+                                               ("SE+WN", 1001, 150, 5), ("SE+SE", 333, 64, 3)])
 def test_fit_predict_dag_vs_oracle(name, n, npred, dim, monkeypatch):
     """gpr_fit_predict with the tile-DAG (GPR_DAG=1): V = U^{-T} [K(x, xp) | y] solved by
     right-hand-side tile tasks of the same persistent launch as the factorisation."""

@@ -18,6 +18,9 @@ HBM before the timed region.
 
 Multi-GPU: the fit does not shard (no distributed Cholesky) -- every rank runs its
 own job ("replicas", weak scaling, no data-path collective); value = jobs/s over all ranks.
+Beside it, key `split_predict`: BASELINE config 5 (split-kernel block prediction, 1M test points)
+SHARDED over all ranks with the RCCL broadcast of U / wt and an all_gather of the shards
+(strong scaling; `--no-split` skips it).
 
 Extra fields: K-build GB/s (8 N^2 / t) and POTRF TFLOP/s ((N^3/3) / t) at N = 32768, stage
 times, and `roofline` for the dominant kernel -- potrf_dag_kernel, the persistent tile-DAG
@@ -97,6 +100,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=8192)
     ap.add_argument("--cpu-np", type=int, default=2048)
+    ap.add_argument("--no-split", action="store_true",
+                    help="skip the C5 split-predict leg (extra key `split_predict`)")
+    ap.add_argument("--split-steps", type=int, default=2)
     return ap.parse_args()
 
 
@@ -161,6 +167,69 @@ def cpu_baseline(a, kinds, hp):
     }
 
 
+class _StdoutToStderr:
+    """RCCL prints its banner and warnings to STDOUT from C; the driver reads ONE JSON line
+    there.  Point file descriptor 1 at stderr while communicators are created and used, and
+    flush C stdio before restoring it."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        try:
+            ctypes.CDLL(None).fflush(None)
+        except OSError:
+            pass
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
+def split_leg(a, world, rank, local):
+    """BASELINE config 5 beside the headline: split-kernel block prediction (ns = 32768, d = 8,
+    SE+WN, 1024 x 1024 test grid, variance for the first 32 grid rows) sharded over all ranks
+    -- rank 0 fits and broadcasts U and wt over RCCL, every rank takes a contiguous block of grid
+    rows, the shards are all-gathered (gpr_amd/distributed.py; bench_split.py is the standalone
+    form).  Strong scaling: fixed total work.  Timed like the headline (warm-up, barrier,
+    max over ranks)."""
+    import gpr_amd as G
+    from gpr_amd.distributed import split_predict_distributed
+
+    ns, d, ne, nq, vr = 32768, 8, 1024, 1024, 32
+    x = np.random.default_rng(0).random((d, ns))
+    y = np.sin(x.sum(0)) ** 2
+    xe = np.random.default_rng(2).random((d, ne))
+    xq = np.random.default_rng(3).random((d, nq))
+    hp = np.r_[1.0, [3.0 * math.sqrt(8.0 / d)] * d, 0.1]
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=G.Context(local))
+    cm = G.Cmap("+", xe, xq)
+    step = lambda: split_predict_distributed(md, cm, var_range=(1, vr), fit="broadcast")  # noqa: E731
+    step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.split_steps):
+        mu, var = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = (time.perf_counter() - t0) / a.split_steps
+    tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    flops = 2.0 * ne * ns * nq + float(nq) * ns * ns * vr
+    return {"metric": "split-predict test points/s (C5)", "value": ne * nq / dt,
+            "unit": "test points/s (whole job)", "ms_per_step": dt * 1e3, "n_gpus": world,
+            "steps": a.split_steps, "scaling": "strong",
+            "workload": f"C5 split predict SE+WN ns={ns} d={d} ne={ne} nq={nq} var_rows={vr} "
+                        f"fit=broadcast, e-row shards x{world}, RCCL broadcast + all_gather",
+            "algorithmic_TFLOPs": flops / dt / 1e12,
+            "results_finite": bool(np.isfinite(mu).all() and np.isfinite(var).all())}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,7 +237,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with _StdoutToStderr():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()  # communicator set up here, banner and all
     import gpr_amd as G
     from gpr_amd import _lib
 
@@ -329,6 +400,20 @@ def main():
             },
             "results_finite": ok,
         }
+    split = None
+    if not a.no_split:
+        try:
+            with _StdoutToStderr():
+                if not dist.is_initialized():  # one rank: a 1-process RCCL group for C5
+                    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                    os.environ.setdefault("MASTER_PORT", "29541")
+                    dist.init_process_group("nccl", rank=0, world_size=1,
+                                            device_id=torch.device("cuda", local))
+                split = split_leg(a, dist.get_world_size(), rank, local)
+        except Exception as ex:  # never let the C5 leg kill the headline line
+            split = {"value": None, "error": repr(ex)}
+    if rank == 0:
+        out["split_predict"] = split
         if not a.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(a, kinds, hp)
@@ -337,9 +422,10 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    if dist.is_initialized():
+        with _StdoutToStderr():
+            dist.barrier()
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -108,7 +108,11 @@ int gpr_kernel_grad(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
  * K = U^T U, strict lower triangle untouched.  *info = 0 or the order of the failing
  * minor.  Replaces cholesky!(Hermitian(K)) = dpotrf('U') (src/cost.jl:77,87,104,
  * src/predict.jl:31).  The context keeps the inverses of the diagonal blocks for the
- * following gpr_potrs/gpr_trsm/gpr_potri calls on the same factor. */
+ * following gpr_potrs/gpr_trsm/gpr_potri calls on the same factor.
+ * Implementation: one persistent tile-DAG launch (128 x 128 tile tasks); n and lda
+ * multiples of 16 with a 128-B aligned dA are factored in place, other shapes on a padded
+ * device copy (n rounded up to 16: an extra ~8 n^2 bytes of device memory, same result);
+ * GPR_DAG=0 in the environment selects the blocked two-stream factorisation. */
 int gpr_potrf_upper(gpr_ctx_t ctx, double* dA, int n, int lda, int* info);
 
 /* B <- K^{-1} B for K = U^T U (dU from gpr_potrf_upper), B n x nrhs (ldb).

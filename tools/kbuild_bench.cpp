@@ -27,37 +27,37 @@ __global__ void store4_kernel(float* p, size_t n) {
 
 // 64 x 64 double tiles in column-major K (ld = N), 512-B column segments, one tile per workgroup
 // iteration: the store shape of the assembly kernels without their math
-__global__ void storetile_kernel(double* K, int N, int ntiles) {
+__global__ void storetile_kernel(double* K, int N, int ntiles, size_t ld) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   const int nt = N / 64, l32 = threadIdx.x & 31, cg = threadIdx.x >> 5;
   for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
     const int bi = b % nt, bj = b / nt;
-    double* base = K + (size_t)bi * 64 + 2 * l32 + ((size_t)bj * 64 + cg) * N;
+    double* base = K + (size_t)bi * 64 + 2 * l32 + ((size_t)bj * 64 + cg) * ld;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)8 * c * N));
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)8 * c * ld));
   }
 }
 
 // TH-row x 64-column tiles, TH/2 lanes of 16 B per column segment
 template <int TH>
-__global__ void storetile_h_kernel(double* K, int N, int ntiles) {
+__global__ void storetile_h_kernel(double* K, int N, int ntiles, size_t ld) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   constexpr int LPC = TH / 2;           // lanes per column
   constexpr int CPI = 256 / LPC;        // columns per instruction
   const int nt = N / TH, lr = threadIdx.x % LPC, cg = threadIdx.x / LPC;
   for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
     const int bi = b % nt, bj = b / nt;
-    double* base = K + (size_t)bi * TH + 2 * lr + ((size_t)bj * 64 + cg) * N;
+    double* base = K + (size_t)bi * TH + 2 * lr + ((size_t)bj * 64 + cg) * ld;
 #pragma unroll
     for (int c = 0; c < 64 / CPI; ++c)
-      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)CPI * c * N));
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)CPI * c * ld));
   }
 }
 
 // the symmetric kernel's write shape: upper 64 x 64 tiles in the kernel's triangular order,
 // each written directly and as its mirror
-__global__ void storepair_kernel(double* K, int N, int ntiles) {
+__global__ void storepair_kernel(double* K, int N, int ntiles, size_t ld) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   const int l32 = threadIdx.x & 31, cg = threadIdx.x >> 5;
   for (int bid = blockIdx.x; bid < ntiles; bid += gridDim.x) {
@@ -65,15 +65,15 @@ __global__ void storepair_kernel(double* K, int N, int ntiles) {
     while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
     while (bj * (bj + 1) / 2 > bid) --bj;
     const int bi = bid - bj * (bj + 1) / 2;
-    double* base = K + (size_t)bi * 64 + 2 * l32 + ((size_t)bj * 64 + cg) * N;
+    double* base = K + (size_t)bi * 64 + 2 * l32 + ((size_t)bj * 64 + cg) * ld;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)8 * c * N));
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)8 * c * ld));
     if (bi == bj) continue;
-    double* mb = K + (size_t)bj * 64 + 2 * l32 + ((size_t)bi * 64 + cg) * N;
+    double* mb = K + (size_t)bj * 64 + 2 * l32 + ((size_t)bi * 64 + cg) * ld;
 #pragma unroll
     for (int c = 0; c < 8; ++c)
-      __builtin_nontemporal_store(d2{3.0, 4.0}, reinterpret_cast<d2*>(mb + (size_t)8 * c * N));
+      __builtin_nontemporal_store(d2{3.0, 4.0}, reinterpret_cast<d2*>(mb + (size_t)8 * c * ld));
   }
 }
 
@@ -81,7 +81,7 @@ __global__ void storepair_kernel(double* K, int N, int ntiles) {
 // column-triangular order, tiles inside column-major; below-diagonal tiles of diagonal
 // super-tiles idle): the active workgroups write S*TH-row runs in both orientations
 template <int TH, int S>
-__global__ void storepair_super_kernel(double* K, int N, int nslots) {
+__global__ void storepair_super_kernel(double* K, int N, int nslots, size_t ld) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   constexpr int LPC = TH / 2, CPI = 256 / LPC;  // lanes per column, columns per instruction
   const int lr = threadIdx.x % LPC, cg = threadIdx.x / LPC;
@@ -93,15 +93,15 @@ __global__ void storepair_super_kernel(double* K, int N, int nslots) {
     const int si = sidx - sj * (sj + 1) / 2;
     const int bi = si * S + loc % S, bj = sj * S + loc / S;
     if (bi > bj) continue;
-    double* base = K + (size_t)bi * TH + 2 * lr + ((size_t)bj * TH + cg) * N;
+    double* base = K + (size_t)bi * TH + 2 * lr + ((size_t)bj * TH + cg) * ld;
 #pragma unroll
     for (int c = 0; c < TH / CPI; ++c)
-      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)CPI * c * N));
+      __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(base + (size_t)CPI * c * ld));
     if (bi == bj) continue;
-    double* mb = K + (size_t)bj * TH + 2 * lr + ((size_t)bi * TH + cg) * N;
+    double* mb = K + (size_t)bj * TH + 2 * lr + ((size_t)bi * TH + cg) * ld;
 #pragma unroll
     for (int c = 0; c < TH / CPI; ++c)
-      __builtin_nontemporal_store(d2{3.0, 4.0}, reinterpret_cast<d2*>(mb + (size_t)CPI * c * N));
+      __builtin_nontemporal_store(d2{3.0, 4.0}, reinterpret_cast<d2*>(mb + (size_t)CPI * c * ld));
   }
 }
 
@@ -136,10 +136,14 @@ int main(int argc, char** argv) {
   srand(1);
   for (auto& v : hx) v = rand() / (double)RAND_MAX;
   for (auto& v : hxp) v = rand() / (double)RAND_MAX;
+  // KB_LDPAD: extra doubles per column of K (ld = N + pad; a power-of-two column stride puts
+  // every column segment of a tile on the same address bits above 256 KB)
+  const size_t ld = (size_t)N + (getenv("KB_LDPAD") ? atoi(getenv("KB_LDPAD")) : 0);
+  printf("N=%d ld=%zu\n", N, ld);
   double *dx, *dxp, *K;
   hipMalloc(&dx, sizeof(double) * hx.size());
   hipMalloc(&dxp, sizeof(double) * hxp.size());
-  hipMalloc(&K, sizeof(double) * (size_t)N * N);
+  hipMalloc(&K, sizeof(double) * (size_t)N * ld);
   hipMemcpy(dx, hx.data(), sizeof(double) * hx.size(), hipMemcpyHostToDevice);
   hipMemcpy(dxp, hxp.data(), sizeof(double) * hxp.size(), hipMemcpyHostToDevice);
   const double l = 3.0 * std::sqrt(8.0 / d);
@@ -202,14 +206,14 @@ int main(int argc, char** argv) {
       timeit([&] { store4_kernel<<<g, 256, 0, s>>>((float*)K, bytes / 4); }, nm);
       const int ntl = (N / 64) * (N / 64);
       snprintf(nm, sizeof nm, "storetile grid %d", g);
-      timeit([&] { storetile_kernel<<<g, 256, 0, s>>>(K, N, ntl); }, nm);
+      timeit([&] { storetile_kernel<<<g, 256, 0, s>>>(K, N, ntl, ld); }, nm);
       snprintf(nm, sizeof nm, "storetile h128 grid %d", g);
-      timeit([&] { storetile_h_kernel<128><<<g, 256, 0, s>>>(K, N, ntl / 2); }, nm);
+      timeit([&] { storetile_h_kernel<128><<<g, 256, 0, s>>>(K, N, ntl / 2, ld); }, nm);
       snprintf(nm, sizeof nm, "storetile h256 grid %d", g);
-      timeit([&] { storetile_h_kernel<256><<<g, 256, 0, s>>>(K, N, ntl / 4); }, nm);
+      timeit([&] { storetile_h_kernel<256><<<g, 256, 0, s>>>(K, N, ntl / 4, ld); }, nm);
       const int ntp = (N / 64) * (N / 64 + 1) / 2;
       snprintf(nm, sizeof nm, "storepair grid %d", g);
-      timeit([&] { storepair_kernel<<<g, 256, 0, s>>>(K, N, ntp); }, nm);
+      timeit([&] { storepair_kernel<<<g, 256, 0, s>>>(K, N, ntp, ld); }, nm);
       snprintf(nm, sizeof nm, "store16x4 grid %d", g);
       timeit([&] { store16x4_kernel<<<g, 256, 0, s>>>(K, bytes / 16); }, nm);
     }
@@ -222,26 +226,26 @@ int main(int argc, char** argv) {
       for (int g : {1024, 2048, 4096}) {
         char nm[64];
         snprintf(nm, sizeof nm, "pair64 S1 grid %d", g);
-        timeit([&] { storepair_super_kernel<64, 1><<<g, 256, 0, s>>>(K, N, slots(64, 1)); }, nm);
+        timeit([&] { storepair_super_kernel<64, 1><<<g, 256, 0, s>>>(K, N, slots(64, 1), ld); }, nm);
         snprintf(nm, sizeof nm, "pair64 S8 grid %d", g);
-        timeit([&] { storepair_super_kernel<64, 8><<<g, 256, 0, s>>>(K, N, slots(64, 8)); }, nm);
+        timeit([&] { storepair_super_kernel<64, 8><<<g, 256, 0, s>>>(K, N, slots(64, 8), ld); }, nm);
         snprintf(nm, sizeof nm, "pair64 S16 grid %d", g);
-        timeit([&] { storepair_super_kernel<64, 16><<<g, 256, 0, s>>>(K, N, slots(64, 16)); }, nm);
+        timeit([&] { storepair_super_kernel<64, 16><<<g, 256, 0, s>>>(K, N, slots(64, 16), ld); }, nm);
         snprintf(nm, sizeof nm, "pair128 S1 grid %d", g);
-        timeit([&] { storepair_super_kernel<128, 1><<<g, 256, 0, s>>>(K, N, slots(128, 1)); }, nm);
+        timeit([&] { storepair_super_kernel<128, 1><<<g, 256, 0, s>>>(K, N, slots(128, 1), ld); }, nm);
         snprintf(nm, sizeof nm, "pair128 S4 grid %d", g);
-        timeit([&] { storepair_super_kernel<128, 4><<<g, 256, 0, s>>>(K, N, slots(128, 4)); }, nm);
+        timeit([&] { storepair_super_kernel<128, 4><<<g, 256, 0, s>>>(K, N, slots(128, 4), ld); }, nm);
         snprintf(nm, sizeof nm, "pair128 S8 grid %d", g);
-        timeit([&] { storepair_super_kernel<128, 8><<<g, 256, 0, s>>>(K, N, slots(128, 8)); }, nm);
+        timeit([&] { storepair_super_kernel<128, 8><<<g, 256, 0, s>>>(K, N, slots(128, 8), ld); }, nm);
         snprintf(nm, sizeof nm, "pair256 S4 grid %d", g);
-        timeit([&] { storepair_super_kernel<256, 4><<<g, 256, 0, s>>>(K, N, slots(256, 4)); }, nm);
+        timeit([&] { storepair_super_kernel<256, 4><<<g, 256, 0, s>>>(K, N, slots(256, 4), ld); }, nm);
       }
     }
     {
       const int ntl = (N / 64) * (N / 64), ntp = (N / 64) * (N / 64 + 1) / 2;
-      timeit([&] { storetile_kernel<<<ntl, 256, 0, s>>>(K, N, ntl); }, "storetile 1 tile/WG");
-      timeit([&] { storetile_h_kernel<128><<<ntl / 2, 256, 0, s>>>(K, N, ntl / 2); }, "storetile h128 1 tile/WG");
-      timeit([&] { storepair_kernel<<<ntp, 256, 0, s>>>(K, N, ntp); }, "storepair 1 tile/WG");
+      timeit([&] { storetile_kernel<<<ntl, 256, 0, s>>>(K, N, ntl, ld); }, "storetile 1 tile/WG");
+      timeit([&] { storetile_h_kernel<128><<<ntl / 2, 256, 0, s>>>(K, N, ntl / 2, ld); }, "storetile h128 1 tile/WG");
+      timeit([&] { storepair_kernel<<<ntp, 256, 0, s>>>(K, N, ntp, ld); }, "storepair 1 tile/WG");
       timeit([&] { store16_kernel<<<(unsigned)(bytes / 16 / 256 / 16), 256, 0, s>>>(K, bytes / 16); }, "store16 16/thread grid-stride");
     }
   }
@@ -259,8 +263,8 @@ int main(int argc, char** argv) {
       float best = 1e30f;
       for (int rep = 0; rep < 4; ++rep) {
         hipEventRecord(e0, s);
-        int rc = cross ? gpr_kernel(ctx, c.kinds.data(), (int)c.kinds.size(), hp.data(), d, dx, N, dxp, M, 0, 1e-8, K, N)
-                       : gpr_kernel(ctx, c.kinds.data(), (int)c.kinds.size(), hp.data(), d, dx, N, nullptr, N, 1, 1e-8, K, N);
+        int rc = cross ? gpr_kernel(ctx, c.kinds.data(), (int)c.kinds.size(), hp.data(), d, dx, N, dxp, M, 0, 1e-8, K, (int)ld)
+                       : gpr_kernel(ctx, c.kinds.data(), (int)c.kinds.size(), hp.data(), d, dx, N, nullptr, N, 1, 1e-8, K, (int)ld);
         hipEventRecord(e1, s);
         hipEventSynchronize(e1);
         if (rc) { printf("rc=%d %s\n", rc, gpr_last_error(ctx)); return 1; }

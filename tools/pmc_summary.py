@@ -74,6 +74,23 @@ def main():
             per = [2.0 * a * 1024.0 + b * 1024.0 for a, b in zip(f1, w1)]
             kernels[k]["traffic_bytes_each_launch"] = per
             kernels[k]["traffic_bytes_max_launch"] = max(per)
+    # MFMA pass (optional): raw counters of each kernel's largest launch (by GRBM_GUI_ACTIVE),
+    # plus BUSY / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs): MFMA-busy cycles per CU-cycle
+    mpat = os.path.join(d, "mfma", "**", "*counter_collection.csv")
+    if glob.glob(mpat, recursive=True):
+        names = set()
+        for f in glob.glob(mpat, recursive=True):
+            names |= {r["Counter_Name"] for r in csv.DictReader(open(f))}
+        lists = {c: per_dispatch_list(mpat, c) for c in sorted(names)}
+        for k in set(lists.get("GRBM_GUI_ACTIVE", {})):
+            g = lists["GRBM_GUI_ACTIVE"][k]
+            i = max(range(len(g)), key=lambda j: g[j])
+            m = {c: lists[c][k][i] for c in lists if k in lists[c] and len(lists[c][k]) == len(g)}
+            busy = m.get("SQ_VALU_MFMA_BUSY_CYCLES")
+            if busy is not None and g[i] > 0:
+                m["mfma_busy_per_cu_cycle"] = busy / (g[i] / 8.0 * 256.0)
+            m["dispatches"] = len(g)
+            kernels.setdefault(k, {})["mfma_largest_launch"] = m
     out = {"config": {"N": n, "np": npred},
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
                      "`bench.py --steps 1 --warmup 0 --no-cpu-baseline`; FETCH_SIZE x2 (gfx950 "

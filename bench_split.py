@@ -46,6 +46,11 @@ def parse():
 
 def main():
     a = parse()
+    # RCCL prints its banner and warnings to STDOUT from C: everything but the one JSON line
+    # goes to stderr (fd 1 points there; the line is written to the saved descriptor)
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -90,7 +95,7 @@ def main():
     mean_flops = 2.0 * a.ne * a.ns * a.nq
     var_flops = float(a.nq) * a.ns * a.ns * (a.var_rows if vr else 0)
     if rank == 0:
-        print(json.dumps({
+        line = json.dumps({
             "metric": "split-predict test points/s (C5: mean + diagonal var rows)",
             "value": npts / dt,
             "unit": "test points/s (whole job)",
@@ -108,7 +113,8 @@ def main():
                        "parallelism": f"e-row shards x{world}, RCCL broadcast + all_gather"},
             "algorithmic_tflop_per_step": (mean_flops + var_flops) / 1e12,
             "results_finite": bool(np.isfinite(mu).all() and np.isfinite(var).all()),
-        }), flush=True)
+        })
+        os.write(json_fd, (line + "\n").encode())
     dist.barrier()
     dist.destroy_process_group()
 

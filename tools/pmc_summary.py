@@ -82,6 +82,11 @@ def main():
         for f in glob.glob(mpat, recursive=True):
             names |= {r["Counter_Name"] for r in csv.DictReader(open(f))}
         lists = {c: per_dispatch_list(mpat, c) for c in sorted(names)}
+        durs = defaultdict(dict)  # kernel -> {dispatch: ns}
+        for f in glob.glob(mpat, recursive=True):
+            for r in csv.DictReader(open(f)):
+                durs[short(r["Kernel_Name"])][int(r["Dispatch_Id"])] = \
+                    int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         for k in set(lists.get("GRBM_GUI_ACTIVE", {})):
             g = lists["GRBM_GUI_ACTIVE"][k]
             i = max(range(len(g)), key=lambda j: g[j])
@@ -89,6 +94,12 @@ def main():
             busy = m.get("SQ_VALU_MFMA_BUSY_CYCLES")
             if busy is not None and g[i] > 0:
                 m["mfma_busy_per_cu_cycle"] = busy / (g[i] / 8.0 * 256.0)
+            dl = [durs[k][x] for x in sorted(durs[k])]
+            if len(dl) == len(g) and dl[i] > 0:
+                m["duration_ns"] = dl[i]
+                m["clock_GHz"] = g[i] / 8.0 / dl[i]  # GRBM_GUI_ACTIVE sums the 8 XCDs
+                if "SQ_INSTS_VALU_MFMA_F64" in m:  # every F64 MFMA here is 16x16x4: 2048 flop
+                    m["mfma_f64_TFLOPs"] = m["SQ_INSTS_VALU_MFMA_F64"] * 2048.0 / dl[i] / 1e3
             m["dispatches"] = len(g)
             kernels.setdefault(k, {})["mfma_largest_launch"] = m
     out = {"config": {"N": n, "np": npred},

@@ -428,7 +428,7 @@ def test_potri_and_trsm(n, dag_solve, monkeypatch):
     assert np.array_equal(Kinv, Kinv.T)
     # trsm: B <- U^{-T} B (>= 128 columns at n % 16 == 0: the solve-only tile-DAG)
     U = sla.cholesky(A, lower=False)
-    for nr in (37, 300):
+    for nr in (37, 300, 260):  # (260: a 4-column last tile)
         B = np.random.default_rng(2).random((n, nr))
         dB = ctx.colmajor(B)
         rc = G._lib.lib.gpr_trsm_upper_trans(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,
@@ -745,10 +745,12 @@ def test_fit_predict_fused_vs_oracle(name, n, npred, dim, nb2, fused, monkeypatc
 
 @pytest.mark.parametrize("name,n,npred,dim", [("SE+WN", 1040, 200, 3), ("SE+SE+WN", 2048, 300, 8),
                                                ("SE+WN", 4112, 130, 4), ("SE", 256, 77, 8),
-                                               ("SE+WN", 1001, 150, 5), ("SE+SE", 333, 64, 3)])
+                                               ("SE+WN", 1001, 150, 5), ("SE+SE", 333, 64, 3),
+                                               ("SE+SE+WN", 2048, 256, 8), ("SE+WN", 1040, 140, 3)])
 def test_fit_predict_dag_vs_oracle(name, n, npred, dim, monkeypatch):
     """gpr_fit_predict with the tile-DAG (GPR_DAG=1): V = U^{-T} [K(x, xp) | y] solved by
-    right-hand-side tile tasks of the same persistent launch as the factorisation."""
+    right-hand-side tile tasks of the same persistent launch as the factorisation (np + 1 =
+    131, 257, 141: a last column tile of 3, 1, 13 columns)."""
     monkeypatch.setenv("GPR_FUSED_RHS", "2")
     monkeypatch.setenv("GPR_DAG", "1")
     kinds = KSETS[name]

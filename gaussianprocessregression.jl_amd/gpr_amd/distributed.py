@@ -9,13 +9,16 @@ wt = K^{-1} y exist, so:
      fit="broadcast": U (N x N) and wt are broadcast from rank 0 over RCCL/xGMI;
      fit="replicate": every rank factorises K itself (no N^2 exchange; the better choice
      when the broadcast of 8N^2 bytes costs more than one K + POTRF on a GPU).
-  2. rank r takes grid rows [lo_r, hi_r) (balanced contiguous split of ne) and computes
-     its mean rows mu[lo:hi, :] and the variance rows of var_range that fall inside
-     (src/split_predict.jl:10-19, :39-53; var_range default 1:3,
-     src/caches/split_kernel.jl:10).  Rows outside var_range keep the prior.
-  3. the shards are all-gathered (mu: (hi-lo) x nq per rank, var: (hi-lo) nq) and
-     reassembled in the reference layouts: mu ne x nq column-major (linear e + q ne),
-     var.diag index e nq + q.
+  2. rank r takes an even share of the var_range rows AND an even share of the other rows
+     (shard_pieces: at most three contiguous pieces of grid rows) and computes their mean
+     rows mu[e, :] and, for var_range rows, the variance (src/split_predict.jl:10-19,
+     :39-53; var_range default 1:3, src/caches/split_kernel.jl:10).  Rows outside
+     var_range keep the prior.  A variance row costs an N^2 triangular solve per test point
+     (N = 32768, nq = 1024: ~1.1e12 flop) against ~1e8 for a mean row, so a plain split of
+     the grid rows would leave every variance row of the default var_range on rank 0.
+  3. the shards are all-gathered (mu: rows x nq per rank, var: rows nq, padded to the
+     largest share) and reassembled in the reference layouts: mu ne x nq column-major
+     (linear e + q ne), var.diag index e nq + q.
 
 The collective sequence (broadcast, then all_gather) is the only data exchange; the
 per-rank compute is a pluggable backend so the distributed logic is tested on CPU with
@@ -33,7 +36,7 @@ import torch.distributed as dist
 from . import core
 from ._lib import GprError, PosDefException, lib
 
-__all__ = ["shard_rows", "HipSplitBackend", "split_predict_distributed"]
+__all__ = ["shard_rows", "shard_pieces", "HipSplitBackend", "split_predict_distributed"]
 
 
 def shard_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -41,6 +44,35 @@ def shard_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
     q, r = divmod(n, world)
     lo = rank * q + min(rank, r)
     return lo, lo + q + (1 if rank < r else 0)
+
+
+def shard_pieces(n: int, world: int, rank: int, v_lo: int = 0, v_hi: int = 0):
+    """Grid rows of `rank` as sorted, disjoint contiguous [lo, hi) pieces: an even share
+    (shard_rows) of the variance rows [v_lo, v_hi), plus an even share of the other rows
+    ([0, v_lo) then [v_hi, n), counted as one sequence).  Over all ranks the pieces
+    partition [0, n)."""
+    v_lo, v_hi = max(0, min(v_lo, n)), max(0, min(v_hi, n))
+    nv = max(v_hi - v_lo, 0)
+    pieces = []
+    if nv:
+        a, b = shard_rows(nv, world, rank)
+        if b > a:
+            pieces.append((v_lo + a, v_lo + b))
+    a, b = shard_rows(n - nv, world, rank)
+    # mean-only index i < v_lo is row i; i >= v_lo is row i + nv
+    if a < min(b, v_lo):
+        pieces.append((a, min(b, v_lo)))
+    lo2, hi2 = max(a, v_lo), b
+    if hi2 > lo2:
+        pieces.append((lo2 + nv, hi2 + nv))
+    pieces.sort()
+    merged = []
+    for lo, hi in pieces:  # adjacent pieces become one call
+        if merged and merged[-1][1] == lo:
+            merged[-1] = (merged[-1][0], hi)
+        else:
+            merged.append((lo, hi))
+    return merged
 
 
 def var_rows(var_range: Optional[Tuple[int, int]], ne: int) -> Tuple[int, int]:
@@ -174,18 +206,28 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
         dist.broadcast(wt, _src(group), group=group)
         _hook(backend, "receive")
 
-    # 2. this rank's grid rows and the var_range rows inside them
-    lo, hi = shard_rows(ne, world, rank)
+    # 2. this rank's grid rows (an even share of the variance rows and of the others) and
+    #    the var_range rows inside them
     v_lo, v_hi = var_rows(var_range, ne)
-    mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+    pieces = [shard_pieces(ne, world, r, v_lo, v_hi) for r in range(world)]
+    rows = [sum(b - a for a, b in p) for p in pieces]
 
-    # 3. pack the shard, all-gather padded shards, reassemble the reference layouts
-    emax = -(-ne // world)
-    mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
-    var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
-    if hi > lo:
-        mu_sh[:, :hi - lo] = mu_full[:, lo:hi]
-        var_sh[:(hi - lo) * nq] = var_full[lo * nq:hi * nq]
+    # 3. pack the rank's rows (piece order), all-gather padded shards, reassemble the
+    #    reference layouts
+    emax = max(max(rows), 1)
+    mu_sh = var_sh = None
+    off = 0
+    for lo, hi in pieces[rank]:
+        mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+        if mu_sh is None:
+            mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
+            var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
+        mu_sh[:, off:off + hi - lo] = mu_full[:, lo:hi]
+        var_sh[off * nq:(off + hi - lo) * nq] = var_full[lo * nq:hi * nq]
+        off += hi - lo
+    if mu_sh is None:  # no rows here (more ranks than rows)
+        mu_sh = torch.zeros(nq, emax, dtype=torch.float64, device=dev)
+        var_sh = torch.zeros(emax * nq, dtype=torch.float64, device=dev)
     mus = [torch.empty_like(mu_sh) for _ in range(world)]
     vars_ = [torch.empty_like(var_sh) for _ in range(world)]
     dist.all_gather(mus, mu_sh, group=group)
@@ -193,8 +235,10 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
     mu = np.empty((nq, ne))
     var = np.empty(ne * nq)
     for r in range(world):
-        a, b = shard_rows(ne, world, r)
-        if b > a:
-            mu[:, a:b] = mus[r][:, :b - a].cpu().numpy()
-            var[a * nq:b * nq] = vars_[r][:(b - a) * nq].cpu().numpy()
+        mr, vr = mus[r].cpu().numpy(), vars_[r].cpu().numpy()
+        off = 0
+        for a, b in pieces[r]:
+            mu[:, a:b] = mr[:, off:off + b - a]
+            var[a * nq:b * nq] = vr[off * nq:(off + b - a) * nq]
+            off += b - a
     return mu.T.copy(), var

@@ -104,6 +104,8 @@ def _worker(rank, world, port, out, ne, nq, var_range, fit):
     (3, 8, 4, (1, 8), "replicate"),     # full var_range, replicated factorisation
     (2, 9, 3, (3, 7), "broadcast"),     # var_range straddling the shard boundary
     (3, 2, 6, (1, 3), "broadcast"),     # more ranks than rows: an empty shard
+    (3, 10, 3, (4, 9), "broadcast"),    # variance rows in the middle: 3-piece shards
+    (4, 9, 2, (1, 3), "replicate"),     # fewer variance rows than ranks
 ])
 def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit):
     port = _free_port()
@@ -179,6 +181,28 @@ def test_shard_rows_partition():
             assert all(parts[r][1] == parts[r + 1][0] for r in range(world - 1))
             sizes = [b - a for a, b in parts]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_pieces_partition_and_balance():
+    """Every row on exactly one rank; variance rows and mean-only rows each split evenly
+    (within one row) -- the variance rows are the expensive ones (an N^2 solve per point)."""
+    for n in range(0, 30):
+        for world in range(1, 9):
+            for v_lo in range(0, n + 1, 3):
+                for v_hi in (v_lo, min(n, v_lo + 1), min(n, v_lo + 5), n):
+                    parts = [gd.shard_pieces(n, world, r, v_lo, v_hi) for r in range(world)]
+                    rows = sorted(e for p in parts for a, b in p for e in range(a, b))
+                    assert rows == list(range(n))
+                    for p in parts:
+                        assert all(a < b for a, b in p)
+                        assert all(p[i][1] < p[i + 1][0] for i in range(len(p) - 1))
+                        assert len(p) <= 3
+                    nv = [sum(1 for a, b in p for e in range(a, b) if v_lo <= e < v_hi) for p in parts]
+                    nm = [sum(b - a for a, b in p) - k for p, k in zip(parts, nv)]
+                    assert max(nv) - min(nv) <= 1 and max(nm) - min(nm) <= 1
+    # the bench's C5 shape: 32 variance rows of 1024 over 8 ranks -> 4 each
+    parts = [gd.shard_pieces(1024, 8, r, 0, 32) for r in range(8)]
+    assert [sum(b - a for a, b in p if a < 32) for p in parts] == [4] * 8
 
 
 def test_var_rows_conversion():

@@ -747,7 +747,9 @@ int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
   const int v0 = std::max(var_lo, e_lo), v1 = std::min(var_hi, e_hi);
   if (v1 > v0) {
     const size_t per_row = (size_t)ns * nq;
-    int Eb = (int)std::max<size_t>(1, ((size_t)1 << 28) / per_row);  // <= 2 GiB of RHS per batch
+    // <= 8 GiB of right-hand sides per batch (C5: 32 rows of ns = 32768, nq = 1024 in one
+    // U^{-T} solve of 32768 columns instead of four of 8192)
+    int Eb = (int)std::max<size_t>(1, ((size_t)1 << 30) / per_row);
     Eb = std::min(Eb, v1 - v0);
     GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per_row * Eb));
     for (int e = v0; e < v1; e += Eb) {

@@ -6,7 +6,8 @@ test grid x_{e,q} = xe_e + xq_q are independent once the training factor U and t
 wt = K^{-1} y exist, so:
 
   1. rank 0 fits: K, POTRF (U), wt                        (src/predict.jl:29-34)
-     fit="broadcast": U (N x N) and wt are broadcast from rank 0 over RCCL/xGMI;
+     fit="broadcast": U's upper triangle (packed by 128-column blocks, ~4N^2 bytes) and
+     wt are broadcast from rank 0 over RCCL/xGMI;
      fit="replicate": every rank factorises K itself (no N^2 exchange; the better choice
      when the broadcast of 8N^2 bytes costs more than one K + POTRF on a GPU).
   2. rank r takes an even share of the var_range rows AND an even share of the other rows
@@ -36,7 +37,8 @@ import torch.distributed as dist
 from . import core
 from ._lib import GprError, PosDefException, lib
 
-__all__ = ["shard_rows", "shard_pieces", "HipSplitBackend", "split_predict_distributed"]
+__all__ = ["shard_rows", "shard_pieces", "pack_upper", "unpack_upper", "HipSplitBackend",
+           "split_predict_distributed"]
 
 
 def shard_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -139,6 +141,32 @@ class HipSplitBackend:
         return mu, var
 
 
+_PACK_NB = 128
+
+
+def _packed_len(n: int, nb: int = _PACK_NB) -> int:
+    return sum((j1 - j0) * j1 for j0, j1 in ((j, min(j + nb, n)) for j in range(0, n, nb)))
+
+
+def pack_upper(U: torch.Tensor, nb: int = _PACK_NB) -> torch.Tensor:
+    """The upper triangle of a column-major n x n factor (tensor row c = column c) by
+    column blocks of nb: block [j0, j1) keeps rows [0, j1) of its columns (the diagonal
+    block whole).  ~n^2/2 elements instead of n^2: what the broadcast has to move."""
+    n = U.shape[0]
+    return torch.cat([U[j0:min(j0 + nb, n), :min(j0 + nb, n)].reshape(-1)
+                      for j0 in range(0, n, nb)]) if n else U.reshape(-1)[:0].clone()
+
+
+def unpack_upper(P: torch.Tensor, U: torch.Tensor, nb: int = _PACK_NB) -> None:
+    """Inverse of pack_upper into U (entries below the diagonal blocks are left as they
+    are: no solve reads them)."""
+    n, off = U.shape[0], 0
+    for j0 in range(0, n, nb):
+        j1 = min(j0 + nb, n)
+        U[j0:j1, :j1] = P[off:off + (j1 - j0) * j1].view(j1 - j0, j1)
+        off += (j1 - j0) * j1
+
+
 def _src(group) -> int:
     return dist.get_global_rank(group, 0) if group is not None else 0
 
@@ -202,7 +230,15 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
         if rank != 0:
             U, wt = backend.empty_fit()
         _hook(backend, "publish")
-        dist.broadcast(U, _src(group), group=group)
+        if world > 1:
+            # the upper triangle only (by 128-column blocks): half the bytes over xGMI
+            n = U.shape[0]
+            P = pack_upper(U) if rank == 0 else torch.empty(_packed_len(n), dtype=U.dtype,
+                                                             device=U.device)
+            dist.broadcast(P, _src(group), group=group)
+            if rank != 0:
+                unpack_upper(P, U)
+            del P
         dist.broadcast(wt, _src(group), group=group)
         _hook(backend, "receive")
 

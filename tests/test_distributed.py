@@ -205,6 +205,19 @@ def test_shard_pieces_partition_and_balance():
     assert [sum(b - a for a, b in p if a < 32) for p in parts] == [4] * 8
 
 
+@pytest.mark.parametrize("n", [0, 1, 5, 127, 128, 129, 300])
+def test_pack_upper_roundtrip(n):
+    """The broadcast's packed upper triangle: round trip restores every entry on or above
+    the diagonal (column-major: tensor row c = column c, upper entries U[c, :c+1])."""
+    U = torch.from_numpy(np.random.default_rng(n).random((n, n)))
+    P = gd.pack_upper(U)
+    assert P.numel() == gd._packed_len(n) <= n * (n + 128) // 2 + 128 * 128
+    V = torch.full((n, n), np.nan, dtype=torch.float64)
+    gd.unpack_upper(P, V)
+    for c in range(n):
+        assert torch.equal(V[c, :c + 1], U[c, :c + 1])
+
+
 def test_var_rows_conversion():
     assert gd.var_rows((1, 3), 10) == (0, 3)        # Julia 1:3 -> [0, 3)
     assert gd.var_rows((1, 3), 2) == (0, 2)         # clamped to ne

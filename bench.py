@@ -192,10 +192,10 @@ class _StdoutToStderr:
 def split_leg(a, world, rank, local):
     """BASELINE config 5 beside the headline: split-kernel block prediction (ns = 32768, d = 8,
     SE+WN, 1024 x 1024 test grid, variance for the first 32 grid rows) sharded over all ranks
-    -- rank 0 fits and broadcasts U and wt over RCCL, every rank takes a contiguous block of grid
-    rows, the shards are all-gathered (gpr_amd/distributed.py; bench_split.py is the standalone
+    -- rank 0 fits and broadcasts U (packed upper triangle) and wt over RCCL, every rank takes
+    an even share of the variance rows and of the mean-only rows, the shards are all-gathered (gpr_amd/distributed.py; bench_split.py is the standalone
     form).  Strong scaling: fixed total work.  Timed like the headline (warm-up, barrier,
-    max over ranks)."""
+    max over ranks).  With more than one rank the fit="replicate" variant is timed too."""
     import gpr_amd as G
     from gpr_amd.distributed import split_predict_distributed
 
@@ -207,27 +207,36 @@ def split_leg(a, world, rank, local):
     hp = np.r_[1.0, [3.0 * math.sqrt(8.0 / d)] * d, 0.1]
     md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=G.Context(local))
     cm = G.Cmap("+", xe, xq)
-    step = lambda: split_predict_distributed(md, cm, var_range=(1, vr), fit="broadcast")  # noqa: E731
-    step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.split_steps):
-        mu, var = step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    dt = (time.perf_counter() - t0) / a.split_steps
-    tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    dt = float(tt.item())
     flops = 2.0 * ne * ns * nq + float(nq) * ns * ns * vr
-    return {"metric": "split-predict test points/s (C5)", "value": ne * nq / dt,
-            "unit": "test points/s (whole job)", "ms_per_step": dt * 1e3, "n_gpus": world,
-            "steps": a.split_steps, "scaling": "strong",
-            "workload": f"C5 split predict SE+WN ns={ns} d={d} ne={ne} nq={nq} var_rows={vr} "
-                        f"fit=broadcast, e-row shards x{world}, RCCL broadcast + all_gather",
-            "algorithmic_TFLOPs": flops / dt / 1e12,
-            "results_finite": bool(np.isfinite(mu).all() and np.isfinite(var).all())}
+
+    def timed(fit):
+        step = lambda: split_predict_distributed(md, cm, var_range=(1, vr), fit=fit)  # noqa: E731
+        step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.split_steps):
+            mu, var = step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = (time.perf_counter() - t0) / a.split_steps
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item()), bool(np.isfinite(mu).all() and np.isfinite(var).all())
+
+    dt, ok = timed("broadcast")
+    out = {"metric": "split-predict test points/s (C5)", "value": ne * nq / dt,
+           "unit": "test points/s (whole job)", "ms_per_step": dt * 1e3, "n_gpus": world,
+           "steps": a.split_steps, "scaling": "strong",
+           "workload": f"C5 split predict SE+WN ns={ns} d={d} ne={ne} nq={nq} var_rows={vr} "
+                       f"fit=broadcast, cost-balanced e-row shards x{world}, RCCL broadcast of "
+                       "U's packed upper triangle + all_gather",
+           "algorithmic_TFLOPs": flops / dt / 1e12, "results_finite": ok}
+    if world > 1:  # every rank refits instead of receiving U (no N^2 exchange)
+        dt_r, ok_r = timed("replicate")
+        out["replicate"] = {"value": ne * nq / dt_r, "ms_per_step": dt_r * 1e3,
+                            "results_finite": ok_r}
+    return out
 
 
 def main():

@@ -76,6 +76,10 @@ struct gpr_ctx {
   // 32768 193 -> 173.4 (67.7 TF/s); C3 fit + predict in one DAG launch 321.8 -> 305.5 ms.
   int dag_mode = 1;
   int dag_nmin = 0, dag_nmax = 1 << 30;
+  int dag_zlag = 2;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
+  int dag_lag_built = -1;
+  bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)
+  int dag_gram = 1;       // K^{-1} += Z^T Z as gram tile tasks of the DAG launch (GPR_DAG_GRAM)
   int dag_solve = 0;      // solves from a finished factor as solve-only DAG launches (GPR_DAG_SOLVE)
   int dag_tail = 12288;  // blocked factorisations (GPR_DAG=0, ineligible sizes) hand their last
                          // <= dag_tail columns to the DAG (GPR_DAG_TAIL; 0 = off)
@@ -221,15 +225,17 @@ struct RhsSpec {
   int ldb;
   int lower_rhs;
   int mode;  // 1: own stream (srhs) beside the trailing updates; 2: main stream after each SYRK
-  // optional: gram (ldg) += X_s^T X_s (upper, columns < the panel end) after each solved
-  // panel X_s of B -- K^{-1} = Z^T Z accumulated panel by panel when B is the identity
+  // optional: gram (ldg) = B^T B -- K^{-1} = Z^T Z when B is the identity: gram tile tasks
+  // of the tile-DAG launch (all of it), or accumulated panel by panel by the blocked path
+  // (X_s^T X_s of each solved panel, upper; potrf_core zeroes it first; the caller mirrors)
   double* gram;
   int ldg;
 };
 // one-launch tile-DAG factorisation (+ B <- U^{-T} B); 1 = shape not eligible, 0 = launched
-enum { DAG_SOLVE = 1, DAG_LOWER = 2 };
+// DAG_GRAM (with DAG_LOWER, B = the identity's Z = U^{-T}): also G = Z^T Z (every tile)
+enum { DAG_SOLVE = 1, DAG_LOWER = 2, DAG_GRAM = 4 };
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
-                     int kglob, hipStream_t st, int flags = 0);
+                     int kglob, hipStream_t st, int flags = 0, double* dG = nullptr, int ldg = 0);
 // true when potrf_core would factor (n, lda, dA) as ONE tile-DAG launch (directly, or for
 // other shapes on a padded copy); dag_shape_ok: the launch takes the shape directly
 bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA);

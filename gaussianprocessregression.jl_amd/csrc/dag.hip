@@ -99,6 +99,9 @@ struct DagArgs {
   int ntasks;
   int lower;     // B is lower triangular (the identity's solve Z = U^{-T}): tile (i, c) exists
                  // for i >= c only and accumulates row blocks [c, i)
+  double* G;     // optional (lower B only): G += B^T B, upper tiles (i <= j), ld ldg --
+  size_t ldg;    // K^{-1} = Z^T Z; tickets >= gbase are these tiles
+  int gbase;
 };
 
 __device__ __forceinline__ int ld_sc1(const int* p) {
@@ -262,6 +265,65 @@ __device__ __attribute__((noinline)) int dag_factor(double* S, double* T, size_t
   return diag2_core<true>(S, Xd, fail, T, lda, mv, kglob, winv);
 }
 
+// A gram task: K^{-1} = Z^T Z tile (i, j), i <= j.  Inlined into the GRAM instance of the
+// kernel only (out of line, the calls' register saves slowed every task by ~2 %; inlined
+// into the one kernel, its second copy of the pipeline cost the plain factorisation ~0.3 %)
+__device__ __forceinline__ void dag_gram_task(const DagArgs& a, int i_, int j_,
+                                                        double* lds, int* s_wait) {
+  // (values steering the loop around the barriers are readfirstlane'd: see the kernel)
+  const int i = __builtin_amdgcn_readfirstlane(i_), j = __builtin_amdgcn_readfirstlane(j_);
+  const int n = __builtin_amdgcn_readfirstlane(a.n), nt = __builtin_amdgcn_readfirstlane(a.nt);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  const int* rhsprog = a.sync + 2 + nt;
+  double* T = a.G + (size_t)i * DT + (size_t)j * DT * a.ldg;
+  const int mv = min(DT, n - i * DT), nv = min(DT, n - j * DT);
+  d4v acc[4][4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = d4v{0.0, 0.0, 0.0, 0.0};
+  const double* Pcol = a.B + (size_t)i * DT * a.ldb;
+  const double* Qcol = a.B + (size_t)j * DT * a.ldb;
+  int done = j;
+  while (done < nt) {
+    const int r = dag_wait(rhsprog + i, rhsprog + j, done, nt, a.info, s_wait);
+    const int nst = (min(r * DT, n) - done * DT) / DTK;  // (the last block may be short)
+    dag_accum(acc, Pcol + (size_t)done * DT, a.ldb, mv, Qcol + (size_t)done * DT, a.ldb, nv, nst,
+              lds);
+    done = r;
+  }
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int mm = wm * 64 + jj * 16 + (lane & 15);
+        if (mm < mv && nn < nv && (i != j || mm <= nn))
+          T[(size_t)mm + (size_t)nn * a.ldg] = acc[ii][jj][r];
+      }
+    }
+  // the mirror (a diagonal tile's strict lower half from its own upper half, so G is
+  // exactly symmetric): each store covers 32 B of 16 columns, and the 4 values of r
+  // fill 128-B lines that the L2 merges before write-back
+  double* Tm = a.G + (size_t)j * DT + (size_t)i * DT * a.ldg;
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+        const int mm = wm * 64 + jj * 16 + (lane & 15);
+        if (mm < mv && nn < nv && (i != j || mm < nn))
+          Tm[(size_t)nn + (size_t)mm * a.ldg] = acc[ii][jj][r];
+      }
+}
+
+template <bool GRAM>
 __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
   // ONE LDS variable: with separate __shared__ scalars the accesses get alias scopes, and
   // the waitcnt pass then made every fragment read wait for ALL in-flight LDS-DMA (an
@@ -298,6 +360,15 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
     DTRACE(1, 1);
     if (t >= a.ntasks) break;
     const unsigned code = __builtin_amdgcn_readfirstlane(a.tasks[t]);  // (a vector load)
+    if (GRAM && t >= a.gbase) {
+      // G_ij = sum_{k >= j} B_ki^T B_kj (i <= j; B lower triangular, so row blocks k < j
+      // of B_kj vanish), row blocks taken as both columns of B finalise them; written to
+      // tile (i, j) and, transposed, to (j, i); no one waits for G, so nothing is published
+      if (!skip) dag_gram_task(a, (code >> 16) & 0x7fff, code & 0xffff, lds, &s_wait);
+      ++p_n;
+      __syncthreads();  // every wave has read s_task before wave 0 takes the next ticket
+      continue;
+    }
     const bool rhs = code >> 31;
     const int i = (code >> 16) & 0x7fff, j = code & 0xffff;
     const bool diag = !rhs && i == j;
@@ -503,24 +574,40 @@ int launch_potrf_dag_padded(gpr_ctx* ctx, double* dA, int n, int lda, double* dB
 // lower triangular, e.g. the identity).  Returns 1 when the shape does not qualify (caller
 // falls back), 0 when launched.
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
-                     int kglob, hipStream_t st, int flags) {
-  const bool solve = flags & DAG_SOLVE, lower = flags & DAG_LOWER;
+                     int kglob, hipStream_t st, int flags, double* dG, int ldg) {
+  const bool solve = flags & DAG_SOLVE, lower = flags & DAG_LOWER, gram = flags & DAG_GRAM;
   if ((solve || lower) && (!dB || kglob)) return 1;
+  if (gram && (!lower || !dG || ldg < n || nrhs != n)) return 1;
   if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || ((uintptr_t)dA & 127) || n > DT * 32767 ||
       kglob % DT)
     return 1;
   if (dB && (nrhs <= 0 || ldb % 16 || ((uintptr_t)dB & 127) || nrhs > DT * 65535)) return 1;
   const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
   GPR_TRY(ensure_winv(ctx, kglob + n, DT));
-  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != flags) {
+  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != flags ||
+      ctx->dag_lag_built != ctx->dag_zlag) {
     std::vector<unsigned> tasks;
-    tasks.reserve((size_t)nt * (nt + 1) / 2 + (size_t)nt * ntr);
+    tasks.reserve((size_t)nt * (nt + 1) + (size_t)nt * ntr);
+    // right-hand-side row i after A's row i + lag: a lower-triangular B's tiles (i, c) near
+    // the diagonal accumulate only i - c row blocks and would otherwise sit waiting for W_i
+    // (the diagonal task of the same row, still accumulating i blocks); the order stays
+    // topological (every dependency of a task has an earlier ticket)
+    const int lag = (lower && !solve) ? std::min(ctx->dag_zlag, nt) : 0;
+    auto rhs_row = [&](int i) {
+      for (int c = 0; c < (lower ? std::min(ntr, i + 1) : ntr); ++c)
+        tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
+    };
     for (int i = 0; i < nt; ++i) {
       if (!solve)
         for (int j = i; j < nt; ++j) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
-      for (int c = 0; c < (lower ? std::min(ntr, i + 1) : ntr); ++c)
-        tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
+      if (i - lag >= 0) rhs_row(i - lag);
     }
+    for (int i = std::max(nt - lag, 0); i < nt; ++i) rhs_row(i);
+    // G's upper tiles last, by column: G_ij sums B's row blocks k >= j, so the low columns
+    // (the longest sums, whose first blocks are final earliest) go first
+    if (gram)
+      for (int j = 0; j < nt; ++j)
+        for (int i = 0; i <= j; ++i) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
     // a previous launch on this context may still be reading the old list (solves do not
     // synchronise): drain the context's stream before freeing it
     if (ctx->dag_tasks) {
@@ -536,6 +623,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_nt = nt;
     ctx->dag_ntr = ntr;
     ctx->dag_flags = flags;
+    ctx->dag_lag_built = ctx->dag_zlag;
   }
   const size_t nsync = 2 + (size_t)nt + ntr;
   if (ctx->dag_sync_cap < nsync) {
@@ -574,15 +662,22 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   a.tasks = ctx->dag_tasks;
   a.ntasks = ctx->dag_ntasks;
   a.lower = lower;
+  a.G = gram ? dG : nullptr;
+  a.ldg = (size_t)(gram ? ldg : 0);
+  a.gbase = gram ? ctx->dag_ntasks - nt * (nt + 1) / 2 : ctx->dag_ntasks;
   const int grid = std::min(ctx->dag_ntasks, ctx->ncu);
   // factorisation n^3/3; U^{-T} B: n^2 per column, ~n^3/3 for a lower-triangular n x n B
   const double flops = (solve ? 0.0 : (double)n * n * n / 3.0) +
-                       (lower ? (double)n * n * n / 3.0 : (double)n * n * (dB ? nrhs : 0));
+                       (lower ? (double)n * n * n / 3.0 : (double)n * n * (dB ? nrhs : 0)) +
+                       (gram ? (double)n * n * n / 3.0 : 0.0);
   {
     hipStream_t ls = ctx->ls;
     ctx->ls = st;  // TimerScope records on ctx->ls
     TimerScope ts(ctx, TC_DAG, flops);
-    potrf_dag_kernel<<<grid, 256, 0, st>>>(a);
+    if (gram)
+      potrf_dag_kernel<true><<<grid, 256, 0, st>>>(a);
+    else
+      potrf_dag_kernel<false><<<grid, 256, 0, st>>>(a);
     ctx->ls = ls;
     LAUNCH_CHECK(ctx);
   }

@@ -1638,8 +1638,10 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
                        (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));
     GPR_TRY(ensure_buf(ctx, &ctx->dpanel_rhs, &ctx->panel_rhs_cap, (size_t)nb2 * rhs->nrhs));
   }
-  if (dag_takes_whole(ctx, n, lda, dA) &&
-      (!rhs || (!rhs->gram && (!rhs->lower_rhs || rhs->nrhs == n)))) {
+  // a gram (K^{-1} += Z^T Z) rides in the DAG launch for the identity's Z only
+  const bool dag_rhs_ok = !rhs || ((!rhs->lower_rhs || rhs->nrhs == n) &&
+                                   (!rhs->gram || (rhs->lower_rhs && ctx->dag_gram)));
+  if (dag_takes_whole(ctx, n, lda, dA) && dag_rhs_ok) {
     // one persistent launch: tiles handed between workgroups by progress counters; shapes the
     // launch does not take directly go through a padded copy
     HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
@@ -1647,11 +1649,14 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     if (dag_shape_ok(n, lda, dA))  // (1 = B's layout not taken directly either)
       rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
                             rhs ? rhs->ldb : 0, 0, ctx->stream,
-                            rhs && rhs->lower_rhs ? DAG_LOWER : 0);
+                            (rhs && rhs->lower_rhs ? DAG_LOWER : 0) |
+                                (rhs && rhs->gram ? DAG_GRAM : 0),
+                            rhs ? rhs->gram : nullptr, rhs ? rhs->ldg : 0);
     if (rc == 1 && (!rhs || !rhs->lower_rhs))
       rc = launch_potrf_dag_padded(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
                                    rhs ? rhs->ldb : 0);
     if (rc < 0) return rc;
+    ctx->gram_full = rc == 0 && rhs && rhs->gram;  // (the DAG wrote every tile of it)
     if (rc == 0) {
       int hinfo = 0;
       HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost,
@@ -1671,6 +1676,10 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     }
   }
   hipStream_t user = ctx->stream;
+  ctx->gram_full = false;
+  if (rhs && rhs->gram)  // accumulated panel by panel below (upper; the caller mirrors)
+    HIP_TRY(ctx, hipMemset2DAsync(rhs->gram, (size_t)rhs->ldg * sizeof(double), 0,
+                                  (size_t)n * sizeof(double), n, user));
   hipStream_t s0 = ctx->smain ? ctx->smain : ctx->stream, s1 = ctx->stream2;
   // with fused right-hand sides the trailing updates may run on a high-priority stream so the
   // (normal-priority) solve only takes CUs the factorisation leaves idle (GPR_RHS_LOWPRIO=1)

@@ -270,13 +270,12 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   // solved, so the N^3/3-flop Gram product fills the chain-bound half of the factorisation
   // instead of running after it
   RhsSpec rhs{Z, n, n, 1, ctx->fused_rhs == 2 ? 2 : 1, nullptr, 0};
-  // auto (-1): when the tile-DAG takes the factorisation, factor (one DAG launch), then Z and
-  // Z^T Z (0; Z as lower-triangular right-hand-side tasks of the DAG launch, 1, measured
-  // slower); otherwise (2) both ride the blocked factorisation's lookahead bubbles
-  const int fuse = ctx->fuse_kinv >= 0 ? ctx->fuse_kinv : (dag_takes_whole(ctx, n, ldk, dK) ? 0 : 2);
+  // auto (-1) = 2: Z and K^{-1} += Z^T Z inside the factorisation -- as right-hand-side and
+  // gram tile tasks of the one tile-DAG launch when the DAG takes it (lower right-hand-side
+  // rows lagged behind A's rows, GPR_DAG_ZLAG), otherwise in the blocked factorisation's
+  // lookahead bubbles.  1: Z alone inside, Z^T Z after; 0: both after the factorisation.
+  const int fuse = ctx->fuse_kinv >= 0 ? ctx->fuse_kinv : 2;
   if (fuse == 2) {
-    HIP_TRY(ctx, hipMemset2DAsync(dKinv, (size_t)ldkinv * sizeof(double), 0,
-                                  (size_t)n * sizeof(double), n, ctx->stream));
     rhs.gram = dKinv;
     rhs.ldg = ldkinv;
   }
@@ -285,7 +284,7 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   if (hinfo != 0) return hinfo;
   GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
   if (!fuse) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
-  if (rhs.gram) return launch_mirror_upper(ctx, dKinv, n, ldkinv);
+  if (rhs.gram) return ctx->gram_full ? 0 : launch_mirror_upper(ctx, dKinv, n, ldkinv);
   return kinv_from_z(ctx, Z, n, dKinv, ldkinv);
 }
 

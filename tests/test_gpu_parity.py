@@ -316,6 +316,36 @@ def test_potrf_dag_not_posdef_info(j, monkeypatch):
     assert info == info_ref == j + 1
 
 
+@pytest.mark.parametrize("gram", ["1", "0"])
+def test_fit_kinv_dag_not_posdef_info(gram, monkeypatch):
+    """A non-PD K under the tile-DAG with Z and gram tasks: info = the failing minor's order,
+    the launch drains (the remaining tasks skip), and the context factors the next matrix."""
+    monkeypatch.setenv("GPR_DAG_GRAM", gram)
+    kinds = KSETS["SE+WN"]
+    dim, n = 4, 1024
+    x, y, _ = O.synthetic(dim, n, 0, seed_train=3)
+    ctx = G.Context(0)
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, Kinv, alpha = ctx.empty(n, n), ctx.empty(n, n), ctx.empty(n)
+    karr = (ctypes.c_int * 2)(1, 2)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    hp = O.default_hp(kinds, dim, noise=0.1)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    # eps = -0.012 on the diagonal: the minor of order 625 fails (mid launch, tile row 4 of 8)
+    for eps, ok in ((-0.012, False), (1e-8, True)):
+        info = ctypes.c_int(-1)
+        rc = G._lib.lib.gpr_fit_kinv(ctx.h, karr, 2, hpp, dim, P(dx), n, P(dy), 1, n, eps, P(K), n,
+                                     P(alpha), P(Kinv), n, ctypes.byref(info))
+        Ko = O.kernel(kinds, hp, x, None, eps=eps)
+        if ok:
+            assert rc == 0 and info.value == 0
+            Uo = sla.cholesky(Ko, lower=False)
+            assert relnorm(ctx.host(Kinv), O.kinv_from_upper(Uo)) < 1e-10
+        else:
+            _, info_ref = sla.lapack.dpotrf(Ko, lower=0)
+            assert info_ref == 625 and rc == info.value == info_ref
+
+
 @pytest.mark.parametrize("j", [0, 5, 127, 128, 200])
 def test_potrf_not_posdef_info(j):
     """Non-PD input: info = order of the failing leading minor (dpotrf / PosDefException)."""
@@ -805,11 +835,13 @@ def test_fit_predict_multi_output_and_reuse():
 
 @pytest.mark.parametrize("fuse", ["2", "1", "0"])
 @pytest.mark.parametrize("n,nb2", [(300, None), (1300, 256), (2100, 1024), (777, 512), (1040, None),
-                                   (2048, None)])
+                                   (2048, None), (4096, None)])
 def test_fit_kinv(n, nb2, fuse, monkeypatch):
     """gpr_fit_kinv = update_cache!(::MllGradCache) (src/cost.jl:83-111): U, alpha and the
     dense K^{-1}, with Z = U^{-T} solved inside the factorisation and K^{-1} = Z^T Z
-    accumulated there panel by panel (fuse=2), Z alone inside (fuse=1), or both after it."""
+    accumulated there (fuse=2: gram tile tasks of the tile-DAG launch at n % 16 == 0 --
+    1040 with a short last row block, 2048, 4096 -- else panel by panel in the blocked
+    factorisation), Z alone inside (fuse=1), or both after it."""
     monkeypatch.setenv("GPR_FUSE_KINV", fuse)
     kinds = KSETS["SE+WN"]
     dim = 4

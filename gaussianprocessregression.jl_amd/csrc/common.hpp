@@ -80,7 +80,7 @@ struct gpr_ctx {
   int dag_lag_built = -1;
   bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)
   int dag_gram = 1;       // K^{-1} += Z^T Z as gram tile tasks of the DAG launch (GPR_DAG_GRAM)
-  int dag_solve = 0;      // solves from a finished factor as solve-only DAG launches (GPR_DAG_SOLVE)
+  int dag_solve = -1;     // solves from a finished factor as solve-only DAG launches (GPR_DAG_SOLVE; -1 auto)
   int dag_tail = 12288;  // blocked factorisations (GPR_DAG=0, ineligible sizes) hand their last
                          // <= dag_tail columns to the DAG (GPR_DAG_TAIL; 0 = off)
   unsigned* dag_tasks = nullptr;

@@ -1961,7 +1961,12 @@ int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols
 
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs) {
-  if (ctx->dag_solve && dag_takes_whole(ctx, n, ldu, dU) && nrhs >= 128 &&
+  // solve-only tile-DAG: GPR_DAG_SOLVE=1 always, 0 never; auto (-1) for the wide solves,
+  // where it measured no slower: C5's variance rows (n = 32768, 32768 right-hand sides) 719
+  // vs 725 ms per job on one box, 714.8 vs 714.9 on another; POTRI's Z at n = 16384 48.9 vs
+  // 49.8 ms.  C3's posterior (8193 right-hand sides: 130.4 vs 127.9 ms) stays blocked.
+  const bool dag_solve = ctx->dag_solve > 0 || (ctx->dag_solve < 0 && n >= 8192 && nrhs >= n);
+  if (dag_solve && dag_takes_whole(ctx, n, ldu, dU) && nrhs >= 128 &&
       (!lower_rhs || nrhs == n)) {
     // the tile-DAG with every tile of U final: only B's tiles are tasks (left-looking, one
     // long-K accumulation per tile, W_i from the factor's block inverses)

@@ -78,6 +78,7 @@ struct gpr_ctx {
   int dag_nmin = 0, dag_nmax = 1 << 30;
   int dag_zlag = 2;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
   int dag_lag_built = -1;
+  bool rhs_solved = false; // the last potrf_core solved its RhsSpec (not dropped by its block sizes)
   bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)
   int dag_gram = 1;       // K^{-1} += Z^T Z as gram tile tasks of the DAG launch (GPR_DAG_GRAM)
   int dag_solve = -1;     // solves from a finished factor as solve-only DAG launches (GPR_DAG_SOLVE; -1 auto)

@@ -1633,6 +1633,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   ctx->sqinv_nb2 = 0;
   GPR_TRY(ensure_winv(ctx, n, nb));
   if (rhs && (nb != 128 || nb2 > 2048 || !ctx->srhs || rhs->nrhs <= 0)) rhs = nullptr;
+  ctx->rhs_solved = rhs != nullptr;  // (callers solve a dropped right-hand side afterwards)
   if (rhs) {
     GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap,
                        (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));

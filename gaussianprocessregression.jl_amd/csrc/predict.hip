@@ -200,7 +200,7 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, co
     GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
     if (info) *info = hinfo;
     if (hinfo != 0) return hinfo;
-    return potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n, /*forward=*/false);
+    return potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n, /*forward=*/!ctx->rhs_solved);
   }
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo));
   if (info) *info = hinfo;
@@ -282,9 +282,10 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, fuse ? &rhs : nullptr));
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
+  const bool solved = fuse && ctx->rhs_solved;
   GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n));
-  if (!fuse) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
-  if (rhs.gram) return ctx->gram_full ? 0 : launch_mirror_upper(ctx, dKinv, n, ldkinv);
+  if (!solved) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, Z, n, n, nullptr, 1));
+  if (solved && rhs.gram) return ctx->gram_full ? 0 : launch_mirror_upper(ctx, dKinv, n, ldkinv);
   return kinv_from_z(ctx, Z, n, dKinv, ldkinv);
 }
 
@@ -339,6 +340,7 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
+  if (!ctx->rhs_solved) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, W, m + nrhs, n, nullptr, 0));
   {
     TimerScope ts(ctx, TC_OTHER, 0.0);
     colgemv_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(W, (size_t)n, n, m, Z, (size_t)n, nrhs,
@@ -688,6 +690,70 @@ int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
   return 0;
 }
 
+// Split factors of grid rows [e_lo, e_lo + E) into ctx->dbig2: per SE part p, A_p (E x nq),
+// BT_p (ns x E), C_p (ns x nq) (src/split_kernel.jl:151-159)
+static int split_build_factors(gpr_ctx* ctx, const KParams& kp, int d, const double* dX, int ns,
+                               const double* dXe, int e_lo, int E, const double* dXq, int nq,
+                               double** A, double** BT, double** C) {
+  const int nse = kp.nse;
+  const size_t szA = (size_t)E * nq, szB = (size_t)ns * E, szC = (size_t)ns * nq;
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)nse * (szA + szB + szC)));
+  *A = ctx->dbig2;
+  *BT = *A + nse * szA;
+  *C = *BT + nse * szB;
+  const size_t nxs = (size_t)nse * d * (ns + E + nq);
+  GPR_TRY(ensure_buf(ctx, &ctx->dxs, &ctx->xs_cap, nxs));
+  double* xs = ctx->dxs;
+  double* xes = xs + (size_t)nse * d * ns;
+  double* xqs = xes + (size_t)nse * d * E;
+  TimerScope ts(ctx, TC_OTHER, 0.0);
+  GPR_TRY(launch_scale_inputs(ctx, kp, dX, ns, xs));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dXe + (size_t)e_lo * d, E, xes));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dXq, nq, xqs));
+  for (int p = 0; p < nse; ++p) {
+    const double s2 = kp.sigma[p] * kp.sigma[p];
+    // A: sigma = 1, SplitDistanceA(xe, xq); B: sigma = 1, Euclidean(xe, x) stored as B^T;
+    // C: sigma, SplitDistanceC(x, xq)
+    GPR_TRY(launch_pair(ctx, 1, d, xes + (size_t)p * d * E, E, xqs + (size_t)p * d * nq, nq, 1.0,
+                        *A + p * szA, 1, E));
+    GPR_TRY(launch_pair(ctx, 0, d, xes + (size_t)p * d * E, E, xs + (size_t)p * d * ns, ns, 1.0,
+                        *BT + p * szB, ns, 1));
+    GPR_TRY(launch_pair(ctx, 2, d, xs + (size_t)p * d * ns, ns, xqs + (size_t)p * d * nq, nq, s2,
+                        *C + p * szC, 1, ns));
+  }
+  return 0;
+}
+
+// mu[e, q] = sum_p A_p[e,q] * (B_p diag(wt) C_p)[e,q] for rows [e_lo, e_lo + E)
+// (src/split_predict.jl:10-19)
+static int split_mean(gpr_ctx* ctx, int nse, const double* A, const double* BT, const double* C,
+                      int ns, int E, int nq, const double* dwt, double* dmu, int e_lo, int ne) {
+  const size_t szA = (size_t)E * nq, szB = (size_t)ns * E, szC = (size_t)ns * nq;
+  for (int p = 0; p < nse; ++p) {
+    GemmArgs g{};
+    g.P = BT + p * szB; g.ldp = ns;
+    g.Q = C + p * szC; g.ldq = ns;
+    g.qscale = dwt;
+    g.E = A + p * szA; g.lde = E;
+    g.C = dmu + e_lo; g.ldc = ne;
+    g.M = E; g.N = nq; g.K = ns;
+    g.alpha = 1.0; g.beta = (p == 0) ? 0.0 : 1.0;
+    GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+  }
+  return 0;
+}
+
+// Kxq columns of grid rows [e, e + nr) (row e - e_lo of the factors), column (e' - e) nq + q
+static int split_kxq(gpr_ctx* ctx, int nse, const double* A, const double* BT, const double* C,
+                     int ns, int nq, int E, int erow, int nr, double* out) {
+  TimerScope ts(ctx, TC_OTHER, 0.0);
+  const size_t total = (size_t)ns * nq * nr;
+  int blocks = (int)std::min<size_t>((total + 255) / 256, 65536);
+  split_kxq_kernel<<<blocks, 256, 0, ctx->stream>>>(nse, A, BT, C, ns, nq, E, erow, nr, out);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
 int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                       const double* dX, int ns, const double* dU, int ldu, const double* dwt,
                       const double* dXe, int ne, const double* dXq, int nq, int e_lo, int e_hi,
@@ -700,46 +766,9 @@ int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
   const int E = e_hi - e_lo;
   if (E == 0) return 0;
   const int nse = kp.nse;
-  // ---- factors for the local rows: A_p (E x nq), BT_p (ns x E), C_p (ns x nq)
-  const size_t szA = (size_t)E * nq, szB = (size_t)ns * E, szC = (size_t)ns * nq;
-  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)nse * (szA + szB + szC)));
-  double* A = ctx->dbig2;
-  double* BT = A + nse * szA;
-  double* C = BT + nse * szB;
-  const size_t nxs = (size_t)nse * d * (ns + E + nq);
-  GPR_TRY(ensure_buf(ctx, &ctx->dxs, &ctx->xs_cap, nxs));
-  double* xs = ctx->dxs;
-  double* xes = xs + (size_t)nse * d * ns;
-  double* xqs = xes + (size_t)nse * d * E;
-  {
-    TimerScope ts(ctx, TC_OTHER, 0.0);
-    GPR_TRY(launch_scale_inputs(ctx, kp, dX, ns, xs));
-    GPR_TRY(launch_scale_inputs(ctx, kp, dXe + (size_t)e_lo * d, E, xes));
-    GPR_TRY(launch_scale_inputs(ctx, kp, dXq, nq, xqs));
-    for (int p = 0; p < nse; ++p) {
-      const double s2 = kp.sigma[p] * kp.sigma[p];
-      // A: sigma = 1, SplitDistanceA(xe, xq); B: sigma = 1, Euclidean(xe, x) stored as B^T;
-      // C: sigma, SplitDistanceC(x, xq)  (src/split_kernel.jl:151-159)
-      GPR_TRY(launch_pair(ctx, 1, d, xes + (size_t)p * d * E, E, xqs + (size_t)p * d * nq, nq, 1.0,
-                          A + p * szA, 1, E));
-      GPR_TRY(launch_pair(ctx, 0, d, xes + (size_t)p * d * E, E, xs + (size_t)p * d * ns, ns, 1.0,
-                          BT + p * szB, ns, 1));
-      GPR_TRY(launch_pair(ctx, 2, d, xs + (size_t)p * d * ns, ns, xqs + (size_t)p * d * nq, nq, s2,
-                          C + p * szC, 1, ns));
-    }
-  }
-  // ---- mean: mu[e, q] = sum_p A_p[e,q] * (B_p diag(wt) C_p)[e,q]  (src/split_predict.jl:10-19)
-  for (int p = 0; p < nse; ++p) {
-    GemmArgs g{};
-    g.P = BT + p * szB; g.ldp = ns;
-    g.Q = C + p * szC; g.ldq = ns;
-    g.qscale = dwt;
-    g.E = A + p * szA; g.lde = E;
-    g.C = dmu + e_lo; g.ldc = ne;
-    g.M = E; g.N = nq; g.K = ns;
-    g.alpha = 1.0; g.beta = (p == 0) ? 0.0 : 1.0;
-    GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
-  }
+  double *A, *BT, *C;
+  GPR_TRY(split_build_factors(ctx, kp, d, dX, ns, dXe, e_lo, E, dXq, nq, &A, &BT, &C));
+  GPR_TRY(split_mean(ctx, nse, A, BT, C, ns, E, nq, dwt, dmu, e_lo, ne));
   // ---- variance: prior everywhere in range, then rows e in [var_lo, var_hi) updated
   const double prior = diag_prior(kinds, nk, hp, d);
   GPR_TRY(launch_fill(ctx, dvar + (size_t)e_lo * nq, (size_t)E * nq, prior));
@@ -753,14 +782,7 @@ int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
     GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per_row * Eb));
     for (int e = v0; e < v1; e += Eb) {
       const int nr = std::min(Eb, v1 - e);
-      {
-        TimerScope ts(ctx, TC_OTHER, 0.0);
-        const size_t total = per_row * nr;
-        int blocks = (int)std::min<size_t>((total + 255) / 256, 65536);
-        split_kxq_kernel<<<blocks, 256, 0, ctx->stream>>>(nse, A, BT, C, ns, nq, E, e - e_lo, nr,
-                                                          ctx->dbig);
-        LAUNCH_CHECK(ctx);
-      }
+      GPR_TRY(split_kxq(ctx, nse, A, BT, C, ns, nq, E, e - e_lo, nr, ctx->dbig));
       GPR_TRY(trsm_ut_core(ctx, dU, ns, ldu, ctx->dbig, nr * nq, ns, dvar + (size_t)e * nq, 0));
     }
   }

@@ -735,6 +735,42 @@ def _fit_predict_dev(ctx, kinds, hp, x, y, xp, mode, nb2=None):
     return ctx.host(K), ctx.host(alpha), ctx.host(mu), ctx.host(var)
 
 
+def test_fused_rhs_dropped_by_block_sizes(monkeypatch):
+    """The blocked factorisation takes fused right-hand sides only for outer blocks up to
+    2048; with a 4096 outer block (GPR_DAG=0) it factors alone and the callers solve after
+    it: fit_predict, fit (y inside) and fit_kinv (Z and K^{-1}) stay exact."""
+    monkeypatch.setenv("GPR_DAG", "0")
+    monkeypatch.setenv("GPR_DAG_TAIL", "0")
+    monkeypatch.setenv("GPR_FUSE_Y", "1")
+    kinds = KSETS["SE+WN"]
+    dim, n, m = 4, 4352, 100
+    x, y, xp = O.synthetic(dim, n, m, seed_train=7, seed_test=8)
+    hp = O.default_hp(kinds, dim, noise=0.1)
+    ctx = G.Context(0)
+    _, alpha, mu, var = _fit_predict_dev(ctx, kinds, hp, x, y, xp, G.GPR_PREDICT_DIAG, 4096)
+    U = sla.cholesky(O.kernel(kinds, hp, x), lower=False)
+    mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+    np.testing.assert_allclose(mu.ravel(), mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-8 * O.diag_prior(kinds, hp, dim))
+    np.testing.assert_allclose(alpha.ravel(), O.cho_solve_upper(U, y), rtol=1e-8,
+                               atol=1e-10 * np.abs(O.cho_solve_upper(U, y)).max())
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, Kinv, a2 = ctx.empty(n, n), ctx.empty(n, n), ctx.empty(n)
+    karr = (ctypes.c_int * 2)(1, 2)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    info = ctypes.c_int(-1)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    assert G._lib.lib.gpr_fit(ctx.h, karr, 2, hpp, dim, P(dx), n, P(dy), 1, n, 1e-8, P(K), n,
+                              P(a2), ctypes.byref(info)) == 0 and info.value == 0
+    np.testing.assert_allclose(ctx.host(a2), O.cho_solve_upper(U, y), rtol=1e-8,
+                               atol=1e-10 * np.abs(O.cho_solve_upper(U, y)).max())
+    assert G._lib.lib.gpr_fit_kinv(ctx.h, karr, 2, hpp, dim, P(dx), n, P(dy), 1, n, 1e-8, P(K),
+                                   n, P(a2), P(Kinv), n, ctypes.byref(info)) == 0
+    assert info.value == 0
+    Ki = ctx.host(Kinv)
+    assert np.array_equal(Ki, Ki.T) and relnorm(Ki, O.kinv_from_upper(U)) < 1e-10
+
+
 @pytest.mark.parametrize("fused", ["1", "2", "0"])
 @pytest.mark.parametrize("name,n,npred,dim,nb2", [
     ("SE+WN", 300, 77, 3, None), ("SE+SE+WN", 1300, 200, 8, 256), ("SE+WN", 1025, 64, 2, 1024),

@@ -268,6 +268,34 @@ def test_potrf_dag(n, monkeypatch):
     assert relnorm(ctx.host(dB), O.cho_solve_upper(U, B)) < 1e-11
 
 
+@pytest.mark.parametrize("n,lda,off", [(1040, 1056, 0), (1040, 1043, 0), (1024, 1048, 8),
+                                       (2048, 2176, 128), (1000, 1024, 0)])
+def test_potrf_dag_leading_dim(n, lda, off, monkeypatch):
+    """The tile-DAG on a block of a larger column-major buffer: lda > n (a multiple of 16:
+    taken directly; 1043: through the padded copy), the block starting `off` doubles into
+    the buffer (8: a base 64 B off the 128-B alignment -> padded copy).  U in the block's upper
+    triangle, its lower triangle and everything outside the block untouched."""
+    monkeypatch.setenv("GPR_DAG", "1")
+    ctx = G.Context(0)
+    A = _spd(n, seed=n + lda)
+    rows = off + lda
+    buf = np.random.default_rng(1).random((rows, n + 1))  # column-major rows x (n + 1)
+    buf[off:off + n, :n] = A
+    dbuf = ctx.colmajor(buf)  # column c at c * rows
+    base = dbuf.data_ptr() + 8 * off
+    info = ctypes.c_int(-7)
+    # the block's columns are `rows` apart: pass lda = rows
+    rc = G._lib.lib.gpr_potrf_upper(ctx.h, ctypes.c_void_p(base), n, rows, ctypes.byref(info))
+    assert rc == 0 and info.value == 0, G._lib.lib.gpr_last_error(ctx.h)
+    out = ctx.host(dbuf)
+    R = out[off:off + n, :n]
+    assert relnorm(np.triu(R), sla.cholesky(A, lower=False)) < 1e-12
+    assert np.array_equal(np.tril(R, -1), np.tril(A, -1))
+    mask = np.ones_like(buf, dtype=bool)
+    mask[off:off + n, :n] = False
+    assert np.array_equal(out[mask], buf[mask])
+
+
 @pytest.mark.parametrize("n,nb2,tail", [(3008, 256, 1024), (2064, 512, 1600), (1040, 256, 1040),
                                          (4096, 1024, 2048)])
 def test_potrf_dag_tail(n, nb2, tail, monkeypatch):

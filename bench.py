@@ -87,6 +87,29 @@ def pmc_traffic(kernels, n, npred, largest=False):
     return None
 
 
+def pmc_mfma(kernel, n, npred):
+    """MFMA-pipe utilisation of the kernel's largest launch from the newest committed PMC
+    summary with an MFMA pass (tools/profile_round.sh: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE
+    / 8 XCDs x 256 CUs x 4 SIMDs), the effective clock, and the summary file).  None if none."""
+    try:
+        files = sorted(f for f in os.listdir(PROFILES) if f.endswith("_pmc_summary.json"))
+    except OSError:
+        return None
+    for f in reversed(files):
+        try:
+            with open(os.path.join(PROFILES, f)) as fh:
+                js = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if js.get("config", {}).get("N") != n or js.get("config", {}).get("np") != npred:
+            continue
+        m = js.get("kernels", {}).get(kernel, {}).get("mfma_largest_launch")
+        if m and "mfma_busy_per_cu_cycle" in m:
+            return {"busy_frac": m["mfma_busy_per_cu_cycle"] / 4.0,
+                    "clock_GHz": m.get("clock_GHz"), "source": f"profiles/{f}"}
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -406,6 +429,8 @@ def main():
                 "launches": g_launch,
                 "avg_launch_us": g_ms * 1e3 / max(g_launch, 1),
                 "flops_per_launch": g_fl / max(g_launch, 1),
+                # rocprof MFMA counters of the same kernel (committed profile of this command)
+                "pmc_mfma": pmc_mfma(dominant[0], N, NP),
             },
             "results_finite": ok,
         }

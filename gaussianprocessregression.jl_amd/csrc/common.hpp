@@ -77,6 +77,8 @@ struct gpr_ctx {
   int dag_mode = 1;
   int dag_nmin = 0, dag_nmax = 1 << 30;
   int dag_zlag = 2;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
+  int dag_rlag = 0;       // other right-hand-side rows after A's row i + lag (GPR_DAG_RLAG;
+                          // 1, 2, 4 measured no faster for C2 / C3)
   int dag_lag_built = -1;
   bool rhs_solved = false; // the last potrf_core solved its RhsSpec (not dropped by its block sizes)
   bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)

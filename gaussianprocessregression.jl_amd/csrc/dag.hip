@@ -585,14 +585,14 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
   GPR_TRY(ensure_winv(ctx, kglob + n, DT));
   if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != flags ||
-      ctx->dag_lag_built != ctx->dag_zlag) {
+      ctx->dag_lag_built != ctx->dag_zlag * 1024 + ctx->dag_rlag) {
     std::vector<unsigned> tasks;
     tasks.reserve((size_t)nt * (nt + 1) + (size_t)nt * ntr);
     // right-hand-side row i after A's row i + lag: a lower-triangular B's tiles (i, c) near
     // the diagonal accumulate only i - c row blocks and would otherwise sit waiting for W_i
     // (the diagonal task of the same row, still accumulating i blocks); the order stays
     // topological (every dependency of a task has an earlier ticket)
-    const int lag = (lower && !solve) ? std::min(ctx->dag_zlag, nt) : 0;
+    const int lag = solve ? 0 : std::min(lower ? ctx->dag_zlag : ctx->dag_rlag, nt);
     auto rhs_row = [&](int i) {
       for (int c = 0; c < (lower ? std::min(ntr, i + 1) : ntr); ++c)
         tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
@@ -623,7 +623,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_nt = nt;
     ctx->dag_ntr = ntr;
     ctx->dag_flags = flags;
-    ctx->dag_lag_built = ctx->dag_zlag;
+    ctx->dag_lag_built = ctx->dag_zlag * 1024 + ctx->dag_rlag;
   }
   const size_t nsync = 2 + (size_t)nt + ntr;
   if (ctx->dag_sync_cap < nsync) {

@@ -1,7 +1,8 @@
 """Parity at BASELINE.json's full sizes through size-independent properties.
 
 The oracle cannot factor N = 32768 in seconds, so at the bench configurations (C3:
-SE+SE+WN, N = 32768, d = 8, np = 8192; C4: SE+WN, N = 16384, d = 16) the HIP path is
+SE+SE+WN, N = 32768, d = 8, np = 8192; C4: SE+WN, N = 16384, d = 16; C5: SE+WN,
+ns = 32768, d = 8, split grid) the HIP path is
 checked through identities that hold at any size (the small-size oracle parity lives in
 test_gpu_parity.py / test_golden.py):
   * solve residual: ||K alpha - y|| <= 1e-11 (||K||_F ||alpha|| + ||y||)   (backward stable)
@@ -14,6 +15,8 @@ test_gpu_parity.py / test_golden.py):
   * MLL = 0.5 (y.alpha + 2 sum log U_ii + N log 2 pi) from the device factor (rel 1e-12);
     LogScale gradient = gradient .* hp (src/cost.jl:60-70); one component against a central
     finite difference (rel 1e-4).
+  * split prediction (C5) against the direct posterior at the same grid points (two device
+    paths that share only the factor), rtol 1e-8
 The matvec / norms here use torch on the device as an independent checker (not the product
 path).
 """
@@ -114,3 +117,27 @@ def test_c4_mll_and_gradient_full_size():
         hp_m[i] -= h
         fd = (G.loss(G.MarginalLikelihood(), hp_p, md) - G.loss(G.MarginalLikelihood(), hp_m, md)) / (2 * h)
         assert fd == pytest.approx(g[i], rel=1e-4)
+
+
+def test_c5_split_predict_full_size():
+    """C5's training size (ns = 32768, d = 8, SE+WN) on a 64 x 1024 grid with two variance
+    rows: the split path (A, B, C factors; src/split_predict.jl) against the direct posterior
+    (K(x, xp) built point by point; src/predict.jl) at the same 2048 grid points -- two
+    independent device paths -- mean rtol 1e-8, variance within 1e-8 of the prior; rows
+    outside var_range keep the prior exactly."""
+    ns, d, ne, nq = 32768, 8, 64, 1024
+    kinds = ["SE", "WN"]
+    hp = _hp(kinds, d)
+    x = np.random.default_rng(0).random((d, ns))
+    y = np.sin(x.sum(0)) ** 2
+    xe = np.random.default_rng(2).random((d, ne))
+    xq = np.random.default_rng(3).random((d, nq))
+    md = G.GPRModel(_cov(kinds), hp, x, y)
+    mu, var = G.predict(md, G.Cmap("+", xe, xq), diagonal_var=True, var_range=(1, 2))
+    prior = O.diag_prior(kinds, hp, d)
+    assert mu.shape == (ne, nq) and np.isfinite(mu).all()
+    assert np.all(var[2 * nq:] == prior)
+    pts = np.concatenate([xe[:, e:e + 1] + xq for e in range(2)], axis=1)  # (e, q) -> e nq + q
+    mu_d, var_d = G.predict(md, pts, diagonal_var=True)
+    np.testing.assert_allclose(mu[:2].ravel(), np.ravel(mu_d), rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var[:2 * nq], np.ravel(var_d), rtol=1e-8, atol=1e-8 * prior)

@@ -3,6 +3,7 @@
 // 4 waves per CU.  Answers: can ONE wave per SIMD keep the f64 matrix pipe full?
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 typedef double d4v __attribute__((ext_vector_type(4)));
 
 template <int NA>
@@ -20,7 +21,11 @@ __global__ __launch_bounds__(256) void peak_kernel(double* out, int iters, doubl
   if (s == 12345.678) out[threadIdx.x] = s;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1]: iteration multiplier (1: ~4 ms per launch; 70: ~300 ms, long enough for the
+  // clock to settle under load); argv[2] = 1: only the 16-accumulator / 1 WG per CU case
+  const int mult = argc > 1 ? atoi(argv[1]) : 1;
+  const bool one = argc > 2 && atoi(argv[2]) == 1;
   hipDeviceProp_t p;
   (void)hipGetDeviceProperties(&p, 0);
   const int cus = p.multiProcessorCount;
@@ -30,8 +35,8 @@ int main() {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   auto run = [&](auto kern, int na) {
-    for (int wgpc = 1; wgpc <= 2; wgpc *= 2) {
-      const int grid = cus * wgpc, iters = 160000 / na;
+    for (int wgpc = 1; wgpc <= (one ? 1 : 2); wgpc *= 2) {
+      const int grid = cus * wgpc, iters = 160000 / na * mult;
       kern<<<grid, 256>>>(out, 10, 1.0, 1.0);
       (void)hipEventRecord(e0);
       kern<<<grid, 256>>>(out, iters, 1.0, 1.0);
@@ -44,9 +49,11 @@ int main() {
              flops / ms / 1e9, ms);
     }
   };
-  run(peak_kernel<2>, 2);
-  run(peak_kernel<4>, 4);
-  run(peak_kernel<8>, 8);
+  if (!one) {
+    run(peak_kernel<2>, 2);
+    run(peak_kernel<4>, 4);
+    run(peak_kernel<8>, 8);
+  }
   run(peak_kernel<16>, 16);
   return 0;
 }

@@ -176,6 +176,12 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
             acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[p][i][h], F[p][4 + j][h], acc[i][j], 0, 0, 0);
   };
   auto step = [&](int s, d2 (&Fc)[DNP][8], d2 (&Fn)[DNP][8]) {
+    // keep the previous stage's MFMAs ahead of this barrier: issued just before it, they run
+    // while the wave waits there (sunk past it, the matrix pipe idles through the wait)
+    __builtin_amdgcn_sched_barrier(0);
+    // the previous step's fragment reads retired before the barrier lets other waves' DMA
+    // overwrite that stage (waited here, after the step's last MFMAs, not right behind them)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
     dag_vmcnt<DVM>();  // own DMA of stage s+1 retired, stage s+2 still in flight
     __builtin_amdgcn_s_barrier();
     issue(s + 3);
@@ -192,7 +198,6 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - DVM - 16 * DNP, 0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
   };
   d2 F0[DNP][8], F1[DNP][8];
   issue(0);

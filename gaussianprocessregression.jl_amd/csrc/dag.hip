@@ -72,9 +72,17 @@ namespace {
 
 constexpr int DT = 128;                     // tile edge
 constexpr int DTK = 16;                     // K rows per pipeline stage
-constexpr int DPB = 4;                      // LDS stages
+#ifndef DAG_DPB
+#define DAG_DPB 4
+#endif
+constexpr int DPB = DAG_DPB;                // LDS stages (DMA DPB - 1 stages ahead)
 constexpr int DSTAGE = (DT + DT) * DTK;     // doubles per stage (P image, then Q)
-constexpr int DLDS = DPB * DSTAGE;          // 16384 doubles = 128 KB
+constexpr int DLDS = DPB * DSTAGE;          // 16384 doubles = 128 KB at DPB = 4
+// the task loop's three LDS ints: after the stages when they fit in the 160 KB, else in the
+// last stage's final 16 bytes -- they are live only between accumulations (every dag_accum
+// ends with a barrier after its last LDS read; the ints are read before the next one starts)
+constexpr int DINT = (DLDS + 2) * 8 <= 160 * 1024 ? DLDS : DLDS - 2;
+constexpr int DALLOC = DINT + 2;
 constexpr int DNCH = DTK / 2;               // 16-B chunks per LDS row
 constexpr int DRPD = 64 / DNCH;             // rows per wave-wide 1-KB DMA
 constexpr int DNDMA = DT / (4 * DRPD);      // DMA instructions per wave per operand
@@ -182,9 +190,9 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
     // the previous step's fragment reads retired before the barrier lets other waves' DMA
     // overwrite that stage (waited here, after the step's last MFMAs, not right behind them)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
-    dag_vmcnt<DVM>();  // own DMA of stage s+1 retired, stage s+2 still in flight
+    dag_vmcnt<DVM * (DPB - 3)>();  // own DMA of stage s+1 retired, s+2.. still in flight
     __builtin_amdgcn_s_barrier();
-    issue(s + 3);
+    issue(s + DPB - 1);
     read_frags(Fn, s + 1);
     mfma_stage(Fc);
 #pragma unroll
@@ -200,10 +208,9 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
     __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - DVM - 16 * DNP, 0);
   };
   d2 F0[DNP][8], F1[DNP][8];
-  issue(0);
-  issue(1);
-  issue(2);
-  dag_vmcnt<2 * DVM>();
+#pragma unroll
+  for (int t = 0; t < DPB - 1; ++t) issue(t);
+  dag_vmcnt<DVM * (DPB - 2)>();
   __builtin_amdgcn_s_barrier();
   read_frags(F0, 0);
   __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -334,10 +341,10 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
   // the waitcnt pass then made every fragment read wait for ALL in-flight LDS-DMA (an
   // s_waitcnt vmcnt(0) per stage: the DMA never ran ahead; accumulation at 0.23 instead of
   // ~0.28 TF/s per CU)
-  __shared__ double lds[DLDS + 2];
-  int& s_task = reinterpret_cast<int*>(lds + DLDS)[0];
-  int& s_skip = reinterpret_cast<int*>(lds + DLDS)[1];
-  int& s_wait = reinterpret_cast<int*>(lds + DLDS)[2];
+  __shared__ double lds[DALLOC];
+  int& s_task = reinterpret_cast<int*>(lds + DINT)[0];
+  int& s_skip = reinterpret_cast<int*>(lds + DINT)[1];
+  int& s_wait = reinterpret_cast<int*>(lds + DINT)[2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w & 1, wn = w >> 1;

@@ -195,6 +195,12 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
     issue(s + DPB - 1);
     read_frags(Fn, s + 1);
     mfma_stage(Fc);
+// instruction order inside a stage (same-box C3 DAG launch, profiles/r02e_ab_dag_sched_
+// variants.txt): 0 (default) 299.8 ms, 1 300.1, 2 313.6, 3 314.1
+#ifndef DAG_SCHED
+#define DAG_SCHED 0
+#endif
+#if DAG_SCHED == 0
 #pragma unroll
     for (int t = 0; t < DVM; ++t) {
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
@@ -206,6 +212,31 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - DVM - 16 * DNP, 0);
+#elif DAG_SCHED == 1  // DMA spread over twice as many MFMAs
+#pragma unroll
+    for (int t = 0; t < DVM; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 8 * DNP; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - 2 * DVM - 16 * DNP, 0);
+#elif DAG_SCHED == 2  // fragment reads first, then the DMA
+#pragma unroll
+    for (int t = 0; t < 8 * DNP; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < DVM; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - 2 * DVM - 8 * DNP, 0);
+#endif  // DAG_SCHED == 3: the compiler's own order
   };
   d2 F0[DNP][8], F1[DNP][8];
 #pragma unroll

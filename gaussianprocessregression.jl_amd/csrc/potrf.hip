@@ -559,7 +559,6 @@ __device__ __forceinline__ void sq_publish(int* prog, int c, int v) {
 // of polling the factorisation is flagged (info = -1) and the wait gives up, so the grid
 // always drains.
 __device__ __forceinline__ void sq_wait(int* prog, int c, int v, int* info) {
-  __shared__ int s_ok;
   if (threadIdx.x == 0) {
     int ok = 1;
     long long spins = 0;
@@ -573,7 +572,6 @@ __device__ __forceinline__ void sq_wait(int* prog, int c, int v, int* info) {
     if (!ok) atomicCAS(info, 0, -1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_ok = ok;
   }
   __syncthreads();
 }

@@ -164,8 +164,11 @@ int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d
 
 /* ---- a5/a6/a7 fused: update_cache!(::MllGradCache) = K, cholesky!, alpha, K^{-1} --------- */
 /* src/cost.jl:83-111 in one call: K into dK (upper -> U, lower keeps K), alpha = K^{-1} y
- * (n x nrhs), dKinv = full symmetric K^{-1} (ldkinv).  Z = U^{-T} is solved inside the
- * factorisation (GPR_FUSE_KINV=0: after it), K^{-1} = Z^T Z.  >0: LAPACK info. */
+ * (n x nrhs), dKinv = full symmetric K^{-1} (ldkinv).  Z = U^{-T} and K^{-1} = Z^T Z are
+ * computed inside the factorisation: as right-hand-side and gram tile tasks of the one
+ * tile-DAG launch (n a multiple of 16, 128-B aligned dK), else in the blocked
+ * factorisation's lookahead bubbles (GPR_FUSE_KINV=1: Z alone inside, 0: both after it).
+ * Device workspace: n^2 doubles for Z.  >0: LAPACK info. */
 int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                  const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
                  double* dK, int ldk, double* dalpha, double* dKinv, int ldkinv, int* info);
@@ -175,7 +178,8 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  * ldiv!(wt, kchol, md.y), then predict! :36-71) in one call: K(x, x) into dK (upper
  * overwritten by U, lower keeps K, as gpr_fit), posterior mean/variance at m test points as
  * gpr_predict.  With mode DIAG/FULL the triangular solve of [K(x, xp) | y] runs inside the
- * factorisation (outer block s solved once panel s of U is final), mu = V^T z with
+ * factorisation (right-hand-side tile tasks of the tile-DAG launch; on the blocked path outer
+ * block s is solved once panel s of U is final), mu = V^T z with
  * V = U^{-T} K(x, xp), z = U^{-T} y; dalpha (optional, n x nrhs) = K^{-1} y.  dwork: optional
  * n*(m+nrhs) doubles.  Returns >0 (LAPACK info) for a non-PD K. */
 int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,

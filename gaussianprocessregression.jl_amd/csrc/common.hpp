@@ -61,13 +61,17 @@ struct gpr_ctx {
   hipStream_t ssq = nullptr;      // square inverses of finished outer panels (fused solves)
   // gpr_fit_predict: 0 = factor, then solve (default); 1 / 2 = solve inside the factorisation
   // on its own stream / on the main stream (GPR_FUSED_RHS; measured slower at C3: 347 vs 334 ms)
-  int fused_rhs = -1;             // gpr_fit_predict: -1 auto (fused, mode 2, for n <=
-                                  // fused_rhs_nmax), 0 off, 1/2 forced (GPR_FUSED_RHS)
+  int fused_rhs = -1;             // gpr_fit_predict: -1 auto (fused, mode 2, when the tile-DAG
+                                  // factors or n <= fused_rhs_nmax), 0 off, 1/2 forced
+                                  // (GPR_FUSED_RHS)
   int fused_rhs_nmax = 16384;     // GPR_FUSED_RHS_NMAX
-  int fuse_y = 0;
-  int fuse_kinv = -1;             // gpr_fit_kinv (-1 auto: 0 when the tile-DAG factors, else 2):
-                                  // Z = U^{-T} solved inside the blocked factorisation
-                                  // (1), and K^{-1} = Z^T Z accumulated there too (2)                 // gpr_fit: forward solve of y inside the factorisation (GPR_FUSE_Y)
+  int fuse_y = 1;                 // gpr_fit: z = U^{-T} y inside the factorisation, then the
+                                  // backward sweep alone (GPR_FUSE_Y=0: both sweeps after it;
+                                  // C5's fit on one GPU: 727 -> 714 ms per job)
+  int fuse_kinv = -1;             // gpr_fit_kinv (GPR_FUSE_KINV; -1 auto = 2): Z = U^{-T} solved
+                                  // inside the factorisation (1), and K^{-1} = Z^T Z too (2) --
+                                  // tile-DAG right-hand-side and gram tasks, or the blocked
+                                  // factorisation's lookahead bubbles
   int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
   int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
   // persistent tile-DAG factorisation (dag.hip): 0 off, 1 on for dag_nmin <= n <= dag_nmax

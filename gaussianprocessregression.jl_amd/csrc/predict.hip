@@ -195,7 +195,8 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, co
                                 (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
   int hinfo = 0;
   if (ctx->fuse_y) {
-    // z = U^{-T} y solved inside the factorisation (side stream), then the backward sweep
+    // z = U^{-T} y solved inside the factorisation (a right-hand-side column of the tile-DAG
+    // launch, or the blocked path's side stream), then the backward sweep
     RhsSpec rhs{dalpha, nrhs, n, 0, ctx->fused_rhs == 2 ? 2 : 1, nullptr, 0};
     GPR_TRY(potrf_core(ctx, dK, n, ldk, &hinfo, &rhs));
     if (info) *info = hinfo;

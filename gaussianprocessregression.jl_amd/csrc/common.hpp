@@ -83,6 +83,8 @@ struct gpr_ctx {
   int dag_zlag = 2;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
   int dag_rlag = 0;       // other right-hand-side rows after A's row i + lag (GPR_DAG_RLAG;
                           // 1, 2, 4 measured no faster for C2 / C3)
+  int dag_fearly = 0;     // diagonal tasks right behind the tile they wait for (GPR_DAG_FEARLY;
+                          // measured C2 -1..0 %, C4 -0.3 %, C3 +0.4 %: off)
   int dag_lag_built = -1;
   bool rhs_solved = false; // the last potrf_core solved its RhsSpec (not dropped by its block sizes)
   bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)

@@ -628,7 +628,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
   GPR_TRY(ensure_winv(ctx, kglob + n, DT));
   if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != flags ||
-      ctx->dag_lag_built != ctx->dag_zlag * 1024 + ctx->dag_rlag) {
+      ctx->dag_lag_built != (ctx->dag_zlag * 1024 + ctx->dag_rlag) * 2 + ctx->dag_fearly) {
     std::vector<unsigned> tasks;
     tasks.reserve((size_t)nt * (nt + 1) + (size_t)nt * ntr);
     // right-hand-side row i after A's row i + lag: a lower-triangular B's tiles (i, c) near
@@ -640,9 +640,20 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
       for (int c = 0; c < (lower ? std::min(ntr, i + 1) : ntr); ++c)
         tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
     };
+    // diagonal tasks early (GPR_DAG_FEARLY): F(i + 1) right behind T(i, i + 1), the one tile
+    // of row i it still needs, instead of behind all of row i -- its factorisation then runs
+    // while row i's other tiles accumulate, and row i + 1's tiles stop waiting for W_{i+1}.
+    // Still topological: F(i + 1) needs T(k, i + 1), k <= i, all on earlier tickets.
+    const bool fearly = ctx->dag_fearly && !solve;
     for (int i = 0; i < nt; ++i) {
-      if (!solve)
-        for (int j = i; j < nt; ++j) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
+      if (!solve) {
+        if (!fearly || i == 0) tasks.push_back(((unsigned)i << 16) | (unsigned)i);
+        for (int j = i + 1; j < nt; ++j) {
+          tasks.push_back(((unsigned)i << 16) | (unsigned)j);
+          if (fearly && j == i + 1)
+            tasks.push_back(((unsigned)j << 16) | (unsigned)j);  // F(i + 1)
+        }
+      }
       if (i - lag >= 0) rhs_row(i - lag);
     }
     for (int i = std::max(nt - lag, 0); i < nt; ++i) rhs_row(i);
@@ -666,7 +677,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_nt = nt;
     ctx->dag_ntr = ntr;
     ctx->dag_flags = flags;
-    ctx->dag_lag_built = ctx->dag_zlag * 1024 + ctx->dag_rlag;
+    ctx->dag_lag_built = (ctx->dag_zlag * 1024 + ctx->dag_rlag) * 2 + ctx->dag_fearly;
   }
   const size_t nsync = 2 + (size_t)nt + ntr;
   if (ctx->dag_sync_cap < nsync) {

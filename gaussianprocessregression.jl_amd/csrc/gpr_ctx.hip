@@ -177,6 +177,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   if (const char* e = getenv("GPR_DAG_GRAM")) ctx->dag_gram = atoi(e);
   if (const char* e = getenv("GPR_DAG_ZLAG")) ctx->dag_zlag = std::max(0, atoi(e));
   if (const char* e = getenv("GPR_DAG_RLAG")) ctx->dag_rlag = std::max(0, atoi(e));
+  if (const char* e = getenv("GPR_DAG_FEARLY")) ctx->dag_fearly = atoi(e) != 0;
   if (const char* e = getenv("GPR_INV_STRIP_MIN")) ctx->inv_strip_min = atoi(e);
   if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
   // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside

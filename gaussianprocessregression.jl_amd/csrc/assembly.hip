@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "kexp.hpp"
 
 namespace {
 
@@ -302,49 +303,6 @@ int scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, doubl
 // read as half-wave broadcasts.  The mirror tile goes through LDS (row stride 65 doubles:
 // conflict-free scalar writes) and is re-read as row pairs, so it too is stored 16 B/lane.
 constexpr int KT_LDS = KT * (KT + 1);  // doubles; also holds the 64 x D column points
-
-#ifndef GPR_EXP32  // 1: 32-entry exp tables (conflict-free LDS gathers, 2 more FMAs)
-#define GPR_EXP32 0
-#endif
-// s2 * exp(-dist) with the part's table ts[j] = s2 * 2^(j/256): the Tang reduction of
-// kexp_neg_tab with magic-constant rounding (kf = x 256/ln2 + 1.5 2^52 holds n = rint(x 256/ln2)
-// in its low word: no rndne / cvt), a degree-4 expm1 (truncation < 0.2 ulp) and sigma^2 folded
-// into the table (one rounding of s2 * T[j]).  16 VALU + 1 LDS read per element.
-__device__ __forceinline__ double kexp_s2(double dist, const double* ts) {
-#ifdef GPR_KBUILD_NOEXP
-  return ts[0] * fma(dist, -1e-3, 1.0);
-#elif GPR_EXP32
-  // 32-entry table 2^(j/32) (every entry in its own LDS bank pair: conflict-free gathers),
-  // |r| <= ln2/64, degree-6 expm1 (truncation < 0.03 ulp); tab[j] = ts[8 j]
-  const double x = dist > 800.0 ? -800.0 : -dist;
-  const double kf = fma(x, 46.16624130844683, 6755399441055744.0);
-  const double nf = kf - 6755399441055744.0;
-  double r = fma(nf, -0.02166084938653512, x);  // ln2/32 = L1 (32 bits) + L2
-  r = fma(nf, -5.9631716539705866e-12, r);
-  const int ni = (int)(unsigned)__double_as_longlong(kf);
-  double p = fma(r, 1.3888888888888889e-03, 8.3333333333333332e-03);
-  p = fma(r, p, 0.041666666666666664);
-  p = fma(r, p, 0.16666666666666666);
-  p = fma(r, p, 0.5);
-  p = r * p;
-  const double q = fma(r, p, r);
-  const double t = ts[ni & 31];
-  return __builtin_ldexp(fma(t, q, t), ni >> 5);
-#else
-  const double x = dist > 800.0 ? -800.0 : -dist;
-  const double kf = fma(x, 369.3299304675746, 6755399441055744.0);
-  const double nf = kf - 6755399441055744.0;
-  double r = fma(nf, -0.00270760617331689, x);
-  r = fma(nf, -7.453964567463233e-13, r);
-  const int ni = (int)(unsigned)__double_as_longlong(kf);
-  double p = fma(r, 0.041666666666666664, 0.16666666666666666);
-  p = fma(r, p, 0.5);
-  p = r * p;
-  const double q = fma(r, p, r);  // expm1(r)
-  const double t = ts[ni & 255];
-  return __builtin_ldexp(fma(t, q, t), ni >> 8);
-#endif
-}
 
 // One 64 x 64 tile of K (or cross K), all SE parts summed in part order (src/compose_covar.jl:
 // 52-56).  DIAG: a diagonal tile of the symmetric K -- eps per SE part and sigma_n^2 on i == j

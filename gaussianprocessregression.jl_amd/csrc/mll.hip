@@ -14,6 +14,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "kexp.hpp"
 
 namespace {
 
@@ -51,12 +52,15 @@ __global__ __launch_bounds__(1024) void mll_terms_kernel(const double* __restric
 }
 
 // partial[bid][slot]: slot layout = for each SE part p: [S_sigma, S_l1..S_ld], then S_wn.
-template <int D>
+// EXACT: d == D (no per-feature bound checks).  Branch-free inner loop: columns past n are
+// clamped to point n - 1 with zero weight, K_p by the K-assembly's table exponential.
+template <int D, bool EXACT>
 __global__ __launch_bounds__(256) void mll_grad_tiles_kernel(KParams kp, const double* __restrict__ X,
                                                              int n, const double* __restrict__ Kinv,
                                                              size_t ldk, const double* __restrict__ alpha,
                                                              double* __restrict__ partial, int nslot) {
   __shared__ double red[4][D + 2];
+  __shared__ double tabs[KMAXP][256];  // sigma_p^2 2^(j/256)
   const int bid = blockIdx.x;
   int bj = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
   while ((bj + 1) * (bj + 2) / 2 <= bid) ++bj;
@@ -65,64 +69,58 @@ __global__ __launch_bounds__(256) void mll_grad_tiles_kernel(KParams kp, const d
   const int i0 = bi * GT, j0 = bj * GT;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int d = kp.d;
+  const int d = EXACT ? D : kp.d;
   const int i = i0 + lane;
   const bool irow = i < n;
   const double wgt = (bi == bj) ? 1.0 : 2.0;
+  for (int p = 0; p < kp.nse; ++p)
+    tabs[p][threadIdx.x] = (kp.sigma[p] * kp.sigma[p]) * kp.exptab[threadIdx.x];
 
-  // M_ab = w (alpha_a alpha_b - Kinv_ab) for this thread's 16 elements
-  double Mv[16];
+  // WhiteNoise term: alpha_a^2 - Kinv_aa from the thread whose columns hold a (diagonal tiles)
   const double ai = irow ? alpha[i] : 0.0;
   double s_wn = 0.0;
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const int j = j0 + wv + 4 * c;
-    double mv = 0.0;
-    if (irow && j < n) {
-      const double kin = Kinv[(size_t)i + (size_t)j * ldk];
-      mv = wgt * (ai * alpha[j] - kin);
-      if (i == j) s_wn += ai * ai - kin;
-    }
-    Mv[c] = mv;
-  }
+  if (bi == bj && irow && ((lane - wv) & 3) == 0) s_wn = ai * ai - Kinv[(size_t)i + (size_t)i * ldk];
 
   double xr[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) xr[k] = (irow && k < d) ? X[(size_t)i * d + k] : 0.0;
+  for (int k = 0; k < D; ++k) xr[k] = (irow && (EXACT || k < d)) ? X[(size_t)i * d + k] : 0.0;
+  __syncthreads();  // tabs
 
   int slot = 0;
   for (int p = 0; p < kp.nse; ++p) {
     double xsr[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) xsr[k] = xr[k] * kp.l[p][k < d ? k : 0];
-    const double s2 = kp.sigma[p] * kp.sigma[p];
+    for (int k = 0; k < D; ++k) xsr[k] = xr[k] * kp.l[p][(EXACT || k < d) ? k : 0];
+    const double* ts = tabs[p];
     double acc_s = 0.0;
     double acc_l[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) acc_l[k] = 0.0;
-#pragma unroll
+    // (not unrolled: unrolled, the wave-uniform point loads of all 16 columns were hoisted
+    // into SGPRs and spilled)
+#pragma unroll 1
     for (int c = 0; c < 16; ++c) {
-      const int j = j0 + wv + 4 * c;
-      if (j < n) {
-        const double* xc = X + (size_t)j * d;
-        double dist = 0.0;
+      const int jr = j0 + wv + 4 * c;
+      const int j = min(jr, n - 1);  // wave-uniform: scalar loads of the point
+      // M_ab = w (alpha_a alpha_b - Kinv_ab), 0 past n
+      const double mv = (irow && jr < n) ? wgt * (ai * alpha[j] - Kinv[(size_t)min(i, n - 1) + (size_t)j * ldk]) : 0.0;
+      const double* xc = X + (size_t)j * d;
+      double dist = 0.0;
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          if (k < d) {
-            const double t = xsr[k] - xc[k] * kp.l[p][k];
-            dist = fma(t, t, dist);
-          }
+      for (int k = 0; k < D; ++k) {
+        if (EXACT || k < d) {
+          const double t = xsr[k] - xc[k] * kp.l[p][k];
+          dist = fma(t, t, dist);
         }
-        double Kp = s2 * exp(-1.0 * dist);
-        if (i == j) Kp += kp.eps;
-        const double mk = Mv[c] * Kp;
-        acc_s += mk;
+      }
+      const double Kp = kexp_s2(dist, ts) + (i == j ? kp.eps : 0.0);
+      const double mk = mv * Kp;
+      acc_s += mk;
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          if (k < d) {
-            const double r = xr[k] - xc[k];
-            acc_l[k] = fma(mk, r * r, acc_l[k]);
-          }
+      for (int k = 0; k < D; ++k) {
+        if (EXACT || k < d) {
+          const double r = xr[k] - xc[k];
+          acc_l[k] = fma(mk, r * r, acc_l[k]);
         }
       }
     }
@@ -170,8 +168,12 @@ __global__ void reduce_partials_kernel(const double* __restrict__ partial, int n
 template <int D>
 int launch_grad_tiles(gpr_ctx* ctx, const KParams& kp, const double* X, int n, const double* Kinv,
                       int ldk, const double* alpha, double* partial, int nslot, long long nblk) {
-  mll_grad_tiles_kernel<D><<<(unsigned)nblk, 256, 0, ctx->stream>>>(kp, X, n, Kinv, (size_t)ldk,
-                                                                      alpha, partial, nslot);
+  if (kp.d == D)
+    mll_grad_tiles_kernel<D, true><<<(unsigned)nblk, 256, 0, ctx->stream>>>(
+        kp, X, n, Kinv, (size_t)ldk, alpha, partial, nslot);
+  else
+    mll_grad_tiles_kernel<D, false><<<(unsigned)nblk, 256, 0, ctx->stream>>>(
+        kp, X, n, Kinv, (size_t)ldk, alpha, partial, nslot);
   LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -899,7 +899,8 @@ def test_fit_predict_multi_output_and_reuse():
 
 @pytest.mark.parametrize("fuse", ["2", "1", "0"])
 @pytest.mark.parametrize("n,nb2", [(300, None), (1300, 256), (2100, 1024), (777, 512), (1040, None),
-                                   (2048, None), (4096, None)])
+                                   (2048, None), (4096, None), (16, None), (144, None),
+                                   (2064, None)])
 def test_fit_kinv(n, nb2, fuse, monkeypatch):
     """gpr_fit_kinv = update_cache!(::MllGradCache) (src/cost.jl:83-111): U, alpha and the
     dense K^{-1}, with Z = U^{-T} solved inside the factorisation and K^{-1} = Z^T Z

@@ -40,6 +40,45 @@ __global__ __launch_bounds__(256) void colgemv_kernel(const double* __restrict__
   }
 }
 
+// The diagonal posterior from V = U^{-T} K(x, xp) and z = U^{-T} y in ONE read of V (one wave
+// per column j): mu[j] = V_j^T z, var[j] = prior - ||V_j||^2 (colgemv + fill + colnorm_sub
+// fused; the order of each sum as in those kernels' lanes, 16-B loads when n is even)
+__global__ __launch_bounds__(256) void colgemv_norm_kernel(const double* __restrict__ V, size_t ldv,
+                                                           int n, int m,
+                                                           const double* __restrict__ z,
+                                                           double prior, double* __restrict__ mu,
+                                                           double* __restrict__ var) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= m) return;
+  const double* col = V + (size_t)j * ldv;
+  double s = 0.0, q = 0.0;
+  int i = 2 * lane;
+  if (((ldv | n) & 1) == 0 && ((uintptr_t)V & 15) == 0 && ((uintptr_t)z & 15) == 0) {
+    for (; i + 1 < n; i += 128) {
+      const d2 v = *reinterpret_cast<const d2*>(col + i);
+      const d2 w = *reinterpret_cast<const d2*>(z + i);
+      s = fma(v.x, w.x, fma(v.y, w.y, s));
+      q = fma(v.x, v.x, fma(v.y, v.y, q));
+    }
+  } else {
+    for (i = lane; i < n; i += 64) {
+      s = fma(col[i], z[i], s);
+      q = fma(col[i], col[i], q);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    q += __shfl_xor(q, o);
+  }
+  if (lane == 0) {
+    mu[j] = s;
+    var[j] = prior - q;
+  }
+}
+
 __global__ void fill_kernel(double* __restrict__ p, size_t n, double v) {
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
        t += (size_t)gridDim.x * blockDim.x)
@@ -342,10 +381,15 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   if (info) *info = hinfo;
   if (hinfo != 0) return hinfo;
   if (!ctx->rhs_solved) GPR_TRY(trsm_ut_core(ctx, dK, n, ldk, W, m + nrhs, n, nullptr, 0));
+  const bool diag1 = mode == GPR_PREDICT_DIAG && nrhs == 1;  // mean and variance in one pass
   {
     TimerScope ts(ctx, TC_OTHER, 0.0);
-    colgemv_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(W, (size_t)n, n, m, Z, (size_t)n, nrhs,
-                                                         dmu, (size_t)m);
+    if (diag1)
+      colgemv_norm_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(
+          W, (size_t)n, n, m, Z, diag_prior(kinds, nk, hp, d), dmu, dvar);
+    else
+      colgemv_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(W, (size_t)n, n, m, Z, (size_t)n,
+                                                           nrhs, dmu, (size_t)m);
     LAUNCH_CHECK(ctx);
   }
   if (dalpha) {
@@ -355,6 +399,7 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
     GPR_TRY(potrs_core(ctx, dK, n, ldk, dalpha, nrhs, n, /*forward=*/false));
   }
   if (mode == GPR_PREDICT_DIAG) {
+    if (diag1) return 0;
     GPR_TRY(launch_fill(ctx, dvar, (size_t)m, diag_prior(kinds, nk, hp, d)));
     return launch_colnorm_sub(ctx, W, n, n, m, dvar);
   }

@@ -126,6 +126,10 @@ def parse():
     ap.add_argument("--no-split", action="store_true",
                     help="skip the C5 split-predict leg (extra key `split_predict`)")
     ap.add_argument("--split-steps", type=int, default=2)
+    # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices by
+    # LOCAL_RANK modulo the device count): gloo carries the collectives (RCCL refuses two
+    # ranks on one device); the driver's runs use the default nccl (= RCCL), one rank per GPU
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     return ap.parse_args()
 
 
@@ -266,11 +270,14 @@ def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
         with _StdoutToStderr():
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if a.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
             dist.barrier()  # communicator set up here, banner and all
     import gpr_amd as G
     from gpr_amd import _lib

@@ -950,6 +950,9 @@ int gpr_kernel(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
   GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
   if (!dX || !dK) return set_err(ctx, GPR_E_ARG, "NULL device pointer");
   if (n < 0) return set_err(ctx, GPR_E_ARG, "n < 0");
+  if (same != GPR_CROSS && same != GPR_SELF && same != GPR_SAME_OBJECT)
+    return set_err(ctx, GPR_E_ARG, "same=%d is not GPR_CROSS, GPR_SELF or GPR_SAME_OBJECT", same);
+  if (same == GPR_SAME_OBJECT) kp.has_noise = 0;  // 5-arg x === xp: eps per SE part, no noise
   if (same) m = n;
   else if (!dXp) return set_err(ctx, GPR_E_ARG, "dXp is NULL for a cross kernel");
   if (ldk < (n > 1 ? n : 1)) return set_err(ctx, GPR_E_ARG, "ldk=%d < n=%d", ldk, n);

@@ -218,6 +218,22 @@ __global__ void shift_upper_kernel(const double* __restrict__ K, size_t ldk, int
   }
 }
 
+// Kxp of predict!/predict_mean! (src/predict.jl:37,43): kernel!(pc.Kxp, covar, hp, xp, md.x),
+// stored transposed here (n x m, ld n).  When the caller passes the training inputs
+// themselves (dXp == dX, the C analogue of `xp === md.x`) the reference's 5-arg kernel! takes
+// its same-object branch: eps once per SE part on the diagonal and NO noise
+// (src/covariance.jl:52-56, src/compose_covar.jl:47-61) -- the symmetric kernel without the
+// WhiteNoise term.  Any other xp is a plain cross kernel (no eps, no noise).
+int launch_cross_or_same(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
+                         const double* dXp, int m, double* out) {
+  if (dXp == dX && m == n) {
+    KParams k5 = kp;
+    k5.has_noise = 0;
+    return launch_kernel_matrix(ctx, k5, dX, n, nullptr, n, 1, out, n);
+  }
+  return launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, out, n);
+}
+
 }  // namespace
 
 extern "C" {
@@ -263,7 +279,7 @@ int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d
     GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)n * m));
     Kpx = ctx->dbig2;
   }
-  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, Kpx, n));  // K(x, xp), n x m
+  GPR_TRY(launch_cross_or_same(ctx, kp, dX, n, dXp, m, Kpx));  // K(x, xp), n x m
   {
     TimerScope ts(ctx, TC_OTHER, 0.0);
     colgemv_kernel<<<(m + 3) / 4, 256, 0, ctx->stream>>>(Kpx, (size_t)n, n, m, dwt, (size_t)n, nrhs,
@@ -372,7 +388,7 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
   }
   double* Z = W + (size_t)n * m;
   GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
-  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, dXp, m, 0, W, n));
+  GPR_TRY(launch_cross_or_same(ctx, kp, dX, n, dXp, m, W));
   HIP_TRY(ctx, hipMemcpy2DAsync(Z, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
                                 (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
   RhsSpec rhs{W, m + nrhs, n, 0, fmode == 2 ? 2 : 1, nullptr, 0};

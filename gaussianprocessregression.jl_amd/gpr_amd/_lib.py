@@ -20,6 +20,9 @@ HEADER = os.path.join(HERE, "..", "..", "include", "gpr_hip.h")
 
 GPR_SE = 1
 GPR_WN = 2
+GPR_CROSS = 0        # gpr_kernel `same`: kernel!(K, cov, hp, x, xp), x !== xp
+GPR_SELF = 1         # kernel!(K, cov, hp, x): eps per SE part + noise
+GPR_SAME_OBJECT = 2  # kernel!(K, cov, hp, x, x), x === xp: eps per SE part, no noise
 GPR_PREDICT_MEAN = 0
 GPR_PREDICT_DIAG = 1
 GPR_PREDICT_FULL = 2

@@ -193,6 +193,7 @@ class GPRModel:
                  ctx: Optional[Context] = None, rng=None):
         if x is None:  # GPRModel(cov, x, y) form: random hp (src/models.jl:32-37)
             raise TypeError("x and y are required")
+        x_obj = x  # the caller's object: predict(md, x) with this same object is `xp === md.x`
         x = np.asarray(x, dtype=np.float64)
         if x.ndim == 1:
             x = x[None, :]
@@ -209,6 +210,7 @@ class GPRModel:
         self.covar = covar
         self.params = params
         self.x = x
+        self._x_obj = x_obj
         self.y = y
         self.train_axis = int(train_axis)
         self.ctx = ctx or default_context()
@@ -256,7 +258,12 @@ def get_sample(md: GPRModel) -> np.ndarray:
 # =========================================================================================
 def kernel(cov: AbstractKernel, hp, x, xp=None, eps: float = EPS_DEFAULT,
            ctx: Optional[Context] = None, out: Optional[torch.Tensor] = None, host: bool = True):
-    """kernel(cov, hp, x[, xp]) -> N x M matrix.  ``xp is None`` is the `x === xp` case."""
+    """kernel(cov, hp, x[, xp]) -> N x M matrix.
+
+    ``xp is None`` is the 4-arg kernel!(K, cov, hp, x): eps per SE part plus the noise of a
+    WhiteNoise part (src/compose_covar.jl:73-77).  ``xp is x`` is the 5-arg call with
+    `x === xp`: eps per SE part, no noise (src/compose_covar.jl:47-61,
+    src/covariance.jl:52-56).  Any other xp is a cross kernel."""
     ctx = ctx or default_context()
     dx = ctx.colmajor(x)
     n = dx.shape[0]
@@ -264,10 +271,12 @@ def kernel(cov: AbstractKernel, hp, x, xp=None, eps: float = EPS_DEFAULT,
     kinds, nk = _kinds_arr(cov)
     hpa, hpp = _hp_arr(hp)
     if xp is None:
-        m, dxp, same = n, None, 1
+        m, dxp, same = n, None, _lib.GPR_SELF
+    elif xp is x:
+        m, dxp, same = n, None, _lib.GPR_SAME_OBJECT
     else:
         dxp = ctx.colmajor(xp)
-        m, same = dxp.shape[0], 0
+        m, same = dxp.shape[0], _lib.GPR_CROSS
     K = out if out is not None else ctx.empty(m, n)
     ctx.check(lib.gpr_kernel(ctx.h, kinds, nk, hpp, d, _ptr(dx), n, _ptr(dxp), m, same, eps,
                              _ptr(K), n), "gpr_kernel")
@@ -466,6 +475,16 @@ def _update_predict_cache(pc, md: GPRModel, eps=EPS_DEFAULT):
         raise PosDefException(info.value)
 
 
+def _dxp(md: GPRModel, xp) -> torch.Tensor:
+    """Test points on the device.  ``xp is md.x`` hands the library the training inputs'
+    own device buffer: pointer identity is how the C ABI sees `xp === md.x`, the
+    reference's same-object branch of kernel!(Kxp, covar, hp, xp, md.x) (src/predict.jl:37,43:
+    eps per SE part on Kxp's diagonal, no noise)."""
+    if xp is md.x or xp is md._x_obj or (isinstance(xp, torch.Tensor) and xp is md._dx):
+        return md.dx()
+    return md.ctx.colmajor(xp)
+
+
 def predict_(mu: Optional[torch.Tensor], Sigma: Optional[torch.Tensor], md: GPRModel, xp,
              pc: GPRPredictCache, diagonal_var: bool, mean_only: bool = False,
              eps: float = EPS_DEFAULT):
@@ -473,7 +492,7 @@ def predict_(mu: Optional[torch.Tensor], Sigma: Optional[torch.Tensor], md: GPRM
     ctx = md.ctx
     kinds, nk = _kinds_arr(md.covar)
     hpa, hpp = _hp_arr(md.params)
-    dxp = ctx.colmajor(xp)
+    dxp = _dxp(md, xp)
     m = dxp.shape[0]
     if pc.Kxp.numel() < m * md.n:
         pc.Kxp = ctx.empty(m, md.n)
@@ -505,7 +524,7 @@ def predict(md: GPRModel, xp, diagonal_var: bool = False, eps: float = EPS_DEFAU
         return _split_predict(md, xp, eps=eps, var_range=var_range)
     ctx = md.ctx
     pc = GPRPredictCache(md, 0)
-    dxp = ctx.colmajor(xp)
+    dxp = _dxp(md, xp)
     m = dxp.shape[0]
     mu = ctx.empty(pc.nrhs, m) if pc.nrhs > 1 else ctx.empty(m)
     Sigma = ctx.empty(m) if diagonal_var else ctx.empty(m, m)

@@ -87,9 +87,17 @@ int gpr_timing_get(gpr_ctx_t ctx, int cls, double* ms, long long* launches, doub
 int gpr_timing_reset(gpr_ctx_t ctx);
 
 /* ---- a2/a3: kernel matrices --------------------------------------------------------- */
-/* K[n x m] (ldk) = kernel(cov, hp, x, xp).  same != 0 means `x === xp`
- * (then dXp is ignored, m must equal n): +eps on the diagonal once per SE part and
- * +sigma_n^2 of the first WhiteNoise part.  same == 0: cross kernel, no eps, no noise.
+/* `same` argument of gpr_kernel: which of the reference's kernel! forms is meant.        */
+#define GPR_CROSS 0       /* kernel!(K, cov, hp, x, xp), x !== xp: no eps, no noise         */
+#define GPR_SELF 1        /* kernel!(K, cov, hp, x) (4-arg): eps per SE part + sigma_n^2 of  */
+                          /* the first WhiteNoise part (add_noise!, src/compose_covar.jl:73) */
+#define GPR_SAME_OBJECT 2 /* kernel!(K, cov, hp, x, xp) with x === xp (5-arg): eps per SE  */
+                          /* part, NO noise (src/compose_covar.jl:47-61, covariance.jl:52-56)*/
+
+/* K[n x m] (ldk) = kernel(cov, hp, x, xp).  same = GPR_SELF or GPR_SAME_OBJECT: dXp is
+ * ignored and m must equal n (the symmetric matrix is written in full).  For a single
+ * SquaredExp the two same-object forms coincide (eps only); they differ for composed
+ * kernels with a WhiteNoise part, where only the 4-arg form adds sigma_n^2.
  * Replaces kernel!(kern, ::SquaredExp, hp, x, xp) src/covariance.jl:49-58,85-95,
  * kernel!(kern::AbstractGPUArray, ...) src/covar_gpu.jl:1-18 and
  * kernel!(kern, ::ComposedKernel, hp, x[, xp]) src/compose_covar.jl:47-77. */
@@ -156,7 +164,11 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
  * prior - ||U^{-T} k_j||^2 (prior sigma^2 or sum of all parts' hp[1]^2, no eps:
  * src/predict.jl:51-71,89-95).  GPR_PREDICT_FULL: + dvar (m x m, ldv) = K(xp,xp) -
  * V^T V (src/predict.jl:42-49,83-87).  dwork: optional device scratch of n*m doubles
- * (NULL: the context allocates it).  Replaces predict!/predict_mean! src/predict.jl. */
+ * (NULL: the context allocates it).  Replaces predict!/predict_mean! src/predict.jl.
+ * Same-object rule: dXp == dX (with m == n) is the C analogue of `xp === md.x`; then
+ * K(xp, x) takes the reference's same-object branch of kernel!(Kxp, covar, hp, xp, md.x)
+ * (src/predict.jl:37,43): eps once per SE part on its diagonal, no noise
+ * (src/covariance.jl:52-56, src/compose_covar.jl:47-61).  Any other dXp: cross kernel. */
 int gpr_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                 const double* dX, int n, const double* dU, int ldu, const double* dwt,
                 int nrhs, const double* dXp, int m, int mode, double eps, double* dmu,
@@ -181,7 +193,8 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  * factorisation (right-hand-side tile tasks of the tile-DAG launch; on the blocked path outer
  * block s is solved once panel s of U is final), mu = V^T z with
  * V = U^{-T} K(x, xp), z = U^{-T} y; dalpha (optional, n x nrhs) = K^{-1} y.  dwork: optional
- * n*(m+nrhs) doubles.  Returns >0 (LAPACK info) for a non-PD K. */
+ * n*(m+nrhs) doubles.  Returns >0 (LAPACK info) for a non-PD K.  dXp == dX: the
+ * same-object rule of gpr_predict (K(xp, x) gets eps per SE part, no noise). */
 int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                     const double* dX, int n, const double* dy, int nrhs, int ldy, double eps,
                     double* dK, int ldk, double* dalpha, const double* dXp, int m, int mode,

@@ -109,13 +109,19 @@ def kernel(kinds: Sequence[str], hp: np.ndarray, x: np.ndarray, xp: np.ndarray |
            eps: float = EPS_DEFAULT) -> np.ndarray:
     """Composed / single kernel matrix.
 
-    kernel!(kern, K::ComposedKernel, hp, x)       src/compose_covar.jl:73-77 (same, + noise)
-    kernel!(kern, K::ComposedKernel, hp, x, xp)   src/compose_covar.jl:47-61 (cross, no noise)
+    kernel!(kern, K::ComposedKernel, hp, x)       src/compose_covar.jl:73-77 (xp None:
+                                                  same object, + noise)
+    kernel!(kern, K::ComposedKernel, hp, x, xp)   src/compose_covar.jl:47-61 (no noise; eps
+                                                  per SE part iff xp is x, i.e. x === xp)
     Summation order: first SE part, then `kern .+= kernel(part_t)` for t = 2.. (each SE
-    part carries its own +eps when same), then add_noise! (:63-71) adds sigma_n^2.
+    part carries its own +eps when same), then add_noise! (:63-71) adds sigma_n^2 -- only
+    in the 4-arg form.  So predict(md, md.x) sees eps (not noise) on Kxp's diagonal
+    (src/predict.jl:37,43), which the reference's interpolation test relies on
+    (test/test_models.jl:17-24).
     """
     d = x.shape[0]
-    same = xp is None
+    noise = xp is None
+    same = noise or xp is x
     xq = x if same else xp
     hps = split_hp(kinds, hp, d)
     se_idx = [i for i, k in enumerate(kinds) if k == SE]   # rm_noise :30-33
@@ -124,7 +130,7 @@ def kernel(kinds: Sequence[str], hp: np.ndarray, x: np.ndarray, xp: np.ndarray |
     K = se_kernel(hps[se_idx[0]], x, xq, same, eps)
     for i in se_idx[1:]:
         K = K + se_kernel(hps[i], x, xq, same, eps)
-    if same and WN in kinds:
+    if noise and WN in kinds:
         nidx = kinds.index(WN)  # findfirst: only the first WhiteNoise counts (:64-68)
         K[np.diag_indices(K.shape[0])] += hps[nidx][0] ** 2
     return K
@@ -258,7 +264,7 @@ def predict(kinds, hp, x, y, xp, diagonal_var=False, eps=EPS_DEFAULT):
     K = kernel(kinds, hp, x, None, eps)
     U = chol_upper(K)
     wt = cho_solve_upper(U, y)                    # ldiv!(pc.wt, kchol, md.y)
-    Kxp = kernel(kinds, hp, xp, x, eps)           # np x N cross kernel (no eps, no noise)
+    Kxp = kernel(kinds, hp, xp, x, eps)           # np x N; eps per SE part iff xp is x
     mu = Kxp @ wt
     V = sla.solve_triangular(U, Kxp.T, trans="T", lower=False, check_finite=False).T  # rdiv!(Kxp,U)
     if diagonal_var:

@@ -8,8 +8,9 @@ test_gpu_parity.py / test_golden.py):
   * solve residual: ||K alpha - y|| <= 1e-11 (||K||_F ||alpha|| + ||y||)   (backward stable)
   * factor backward error on sampled entries: |(U^T U)_ij - K_ij| <= 1e-12 ||U_:i|| ||U_:j||,
     K_ij from the oracle's formula for the two points
-  * posterior mean at the training points: mu = K_f alpha = y - (sigma_n^2 + n_SE eps) alpha
-    (the cross kernel carries no jitter/noise, src/predict.jl:37; src/covariance.jl:49-58),
+  * posterior mean at a copy of some training points: mu = y - (sigma_n^2 + n_SE eps) alpha
+    (a cross kernel carries no jitter/noise, src/predict.jl:37; src/covariance.jl:49-58), and
+    at the model's own x (same object): mu = y - sigma_n^2 alpha (eps per SE part on Kxp),
     normwise 1e-9
   * 0 <= diagonal variance <= prior (+ 1e-8 prior)
   * MLL = 0.5 (y.alpha + 2 sum log U_ii + N log 2 pi) from the device factor (rel 1e-12);
@@ -82,6 +83,12 @@ def test_c3_fit_and_posterior_full_size():
     a_h = alpha.cpu().numpy()
     expect = y[sub] - (0.1 ** 2 + 2 * O.EPS_DEFAULT) * a_h[sub]
     assert np.linalg.norm(mu_t - expect) <= 1e-9 * np.linalg.norm(expect)
+    # with the model's OWN x (xp === md.x) Kxp takes the same-object branch: eps per SE part,
+    # no noise (src/predict.jl:37,43; src/compose_covar.jl:47-61), so mu = y - sigma_n^2 alpha
+    mu_s = G.predict_mean(md, md.x)
+    expect_s = y - 0.1 ** 2 * a_h
+    assert np.linalg.norm(mu_s - expect_s) <= 1e-9 * np.linalg.norm(expect_s)
+    del mu_s
     # diagonal variance bounds at the bench's test points
     mu, var = G.predict(md, xp, diagonal_var=True)
     prior = O.diag_prior(kinds, hp, d)

@@ -604,30 +604,90 @@ def test_predict_vs_oracle(name, n, npred, dim):
     np.testing.assert_allclose(G.predict_mean(md, xp), mu_o, rtol=1e-8, atol=1e-10)
 
 
-def test_predict_interpolation_and_diag_vs_full():
-    """test/test_models.jl:17-48.  The reference draws hp at random; the interpolation KAT is
-    only meaningful where K is well conditioned, so length-scale multipliers are chosen per
-    dimension (for d=1 the points are a jittered grid: uniform draws can nearly coincide)."""
-    rng = np.random.default_rng(12)
-    for n, npred, dim, l in [(100, 100, 1, 40.0), (200, 200, 2, 14.0), (500, 100, 5, 5.0)]:
-        x, xp = rng.random((dim, n)), rng.random((dim, npred))
-        if dim == 1:
-            x = (np.arange(n) + 0.5 * rng.random(n))[None, :] / n
-        y = np.sin(x.sum(0)) ** 2
-        hp2 = np.r_[1.0, [l] * dim, 0.8, [1.25 * l] * dim]
-        md2 = G.GPRModel(G.SquaredExp() + G.SquaredExp(), hp2, x, y)
-        mu2 = G.predict_mean(md2, x)  # Julia `≈` on arrays is normwise
-        assert np.linalg.norm(mu2 - y) <= 1e-7 * np.linalg.norm(y)
-        _, S = G.predict(md2, x)
-        assert np.abs(S).max() <= 1e-7
-        md3 = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), np.r_[1.0, [l] * dim, 1e-5], x, y)
-        assert np.linalg.norm(G.predict_mean(md3, x) - y) <= 1e-3 * np.linalg.norm(y)
-        _, S3 = G.predict(md3, x)
-        assert np.abs(S3).max() <= 1e-3
-        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), rng.random(dim + 2) + 0.5, x, y)
-        _, Sf = G.predict(md, xp)
-        _, Sd = G.predict(md, xp, diagonal_var=True)
-        np.testing.assert_allclose(np.diag(Sf), Sd, atol=1e-5)
+@pytest.mark.parametrize("n", [100, 200, 500])
+@pytest.mark.parametrize("npred", [100, 200, 500])
+@pytest.mark.parametrize("dim", [1, 2, 5])
+def test_predict_interpolation_random_hp(n, npred, dim):
+    """test/test_models.jl:1-31 verbatim: GPRModel(cov, x, y) draws hp = rand(D)
+    (src/models.jl:32-37, here seeded), then predict_mean(md2, x) ≈ y rtol 1e-7 and
+    predict(md2, x)'s full Sigma ≈ 0 atol 1e-7 with x the model's OWN input: the same-object
+    branch of kernel!(Kxp, covar, hp, xp, md.x) (src/predict.jl:37,43) puts eps per SE part
+    on Kxp, so Kxp equals K and mu = y up to the solve's backward error for any hp."""
+    rng = np.random.default_rng(1000 * n + 10 * npred + dim)
+    x = rng.random((dim, n))
+    xp = rng.random((dim, npred))
+    y = np.sin(x.sum(0)) ** 2
+    md2 = G.GPRModel(G.SquaredExp() + G.SquaredExp(), None, x, y, rng=rng)
+    assert julia_approx(G.predict_mean(md2, x), y, rtol=1e-7)
+    mu2, S = G.predict(md2, x)
+    assert julia_approx(mu2, y, rtol=1e-7)
+    assert np.abs(S).max() <= 1e-7
+    _, Sd = G.predict(md2, x, diagonal_var=True)
+    assert np.abs(Sd).max() <= 1e-7
+    md3 = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), None, x, y, rng=rng)
+    md3.params[-1] = 1e-5
+    assert julia_approx(G.predict_mean(md3, x), y, rtol=1e-3)
+    _, S3 = G.predict(md3, x)
+    assert np.abs(S3).max() <= 1e-3
+    # the same-object rule is exactly the oracle's (xp is x), for mean and both variances
+    for md, kinds in ((md2, [SE, SE]), (md3, [SE, WN])):
+        mu_o, S_o = O.predict(kinds, md.params, x, y, x)
+        mu_d, S_d = G.predict(md, x)
+        scale = np.linalg.norm(y)
+        assert np.linalg.norm(mu_d - mu_o) <= 1e-7 * scale
+        assert np.abs(S_d - S_o).max() <= 1e-7
+    # a different object with equal values is a cross kernel (no eps): predict(md, copy(x))
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), np.r_[1.0, [3.0] * dim, 0.1], x, y)
+    mu_c = G.predict_mean(md, x.copy())
+    mu_o = O.predict([SE, WN], md.params, x, y, x.copy(), diagonal_var=True)[0]
+    np.testing.assert_allclose(mu_c, mu_o, rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["SE", "SE+WN", "SE+SE+WN", "WN+SE"])
+@pytest.mark.parametrize("diag", [True, False])
+def test_predict_same_object_vs_oracle(name, diag):
+    """predict(md, md.x) with well-conditioned hp against the oracle's same-object rule, on the
+    fused tile-DAG path (n a multiple of 16) and the padded one."""
+    kinds = KSETS[name]
+    for n, dim in ((256, 3), (250, 2)):
+        x, y, _ = O.synthetic(dim, n, 0, seed_train=n)
+        hp = O.default_hp(kinds, dim)
+        md = G.GPRModel(cov_of(kinds), hp, x, y)
+        mu, S = G.predict(md, md.x, diagonal_var=diag)
+        mu_o, S_o = O.predict(kinds, hp, x, y, x, diagonal_var=diag)
+        vtol = 1e-8 * O.diag_prior(kinds, hp, dim)
+        np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+        np.testing.assert_allclose(S, S_o, rtol=1e-8, atol=vtol)
+        if WN in kinds:  # mu = y - sigma_n^2 alpha exactly (Kxp = K - sigma_n^2 I)
+            alpha = O.cho_solve_upper(O.chol_upper(O.kernel(kinds, hp, x)), y)
+            sn = O.split_hp(kinds, hp, dim)[kinds.index(WN)][0]
+            np.testing.assert_allclose(mu, y - sn ** 2 * alpha, rtol=1e-8, atol=1e-10)
+
+
+def test_kernel_same_object_forms():
+    """gpr_kernel's `same` argument: GPR_SELF = 4-arg kernel!(K, cov, hp, x) (eps + noise),
+    GPR_SAME_OBJECT = 5-arg with x === xp (eps per SE part, no noise; src/compose_covar.jl:47-61),
+    and an invalid value is rejected."""
+    rng = np.random.default_rng(31)
+    dim, n = 4, 160
+    x = rng.random((dim, n))
+    for name in ("SE", "SE+WN", "SE+SE+WN", "WN+SE", "SE+WN+SE"):
+        kinds = KSETS[name]
+        hp = rand_hp(kinds, dim, rng)
+        cov = cov_of(kinds)
+        np.testing.assert_allclose(G.kernel(cov, hp, x, x), O.kernel(kinds, hp, x, x),
+                                   rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(G.kernel(cov, hp, x), O.kernel(kinds, hp, x),
+                                   rtol=1e-13, atol=1e-15)
+    ctx = G.default_context()
+    dx = ctx.colmajor(x)
+    K = ctx.empty(n, n)
+    kinds_c = (ctypes.c_int * 1)(1)
+    hp = np.r_[1.0, [1.0] * dim]
+    rc = G._lib.lib.gpr_kernel(ctx.h, kinds_c, 1, hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                               dim, ctypes.c_void_p(dx.data_ptr()), n, None, n, 3, 1e-8,
+                               ctypes.c_void_p(K.data_ptr()), n)
+    assert rc == -1  # GPR_E_ARG
 
 
 def test_predict_multi_output_y():

@@ -103,17 +103,54 @@ def test_compose_identities():
         O.kernel([SE], hps[:dim + 1], x) + O.kernel([SE], hps[dim + 2:], x) + hps[dim + 1] ** 2 * np.eye(n))
 
 
+def test_same_object_kernel_forms():
+    """src/compose_covar.jl:47-77, src/covariance.jl:49-58: the 5-arg kernel! with x === xp
+    adds eps once per SE part and NO noise; the 4-arg form adds the noise too; a different
+    object (even with equal values) gets neither."""
+    rng = np.random.default_rng(21)
+    dim, n = 3, 40
+    x = rng.random((dim, n))
+    for kinds in ([SE, WN], [SE, SE, WN], [WN, SE], [SE, WN, SE], [SE, SE]):
+        hp = rng.random(sum(O.dim_hp(k, dim) for k in kinds))
+        hps = O.split_hp(kinds, hp, dim)
+        se_sum = sum(O.se_kernel(h, x, x, True) for k, h in zip(kinds, hps) if k == SE)
+        noise = sum(h[0] ** 2 for k, h in zip(kinds, hps) if k == WN)
+        np.testing.assert_array_equal(O.kernel(kinds, hp, x, x), se_sum)
+        np.testing.assert_allclose(O.kernel(kinds, hp, x), se_sum + noise * np.eye(n), rtol=1e-15)
+        cross = O.kernel(kinds, hp, x, x.copy())
+        nse = kinds.count(SE)
+        np.testing.assert_allclose(np.diag(O.kernel(kinds, hp, x, x)) - np.diag(cross),
+                                   nse * O.EPS_DEFAULT, rtol=1e-6)
+
+
+@pytest.mark.parametrize("n", [100, 200, 500])
+@pytest.mark.parametrize("npred", [100, 200, 500])
+@pytest.mark.parametrize("dim", [1, 2, 5])
+def test_interpolation_random_hp_verbatim(n, npred, dim):
+    """test/test_models.jl:1-31 verbatim: x = rand(dim, n), y = sin(sum x)^2, and
+    GPRModel(cov, x, y) draws hp = rand(D) (src/models.jl:32-37).  predict_mean(md2, x) with
+    the model's OWN x takes the same-object branch (eps per SE part on Kxp), so mu = y up to
+    the solve's backward error even for the ill-conditioned random hp."""
+    rng = np.random.default_rng(1000 * n + 10 * npred + dim)
+    x = rng.random((dim, n))
+    y = np.sin(x.sum(0)) ** 2
+    hp2 = rng.random(2 * (dim + 1))
+    mu, S = O.predict([SE, SE], hp2, x, y, x)
+    assert np.linalg.norm(mu - y) <= 1e-7 * max(np.linalg.norm(mu), np.linalg.norm(y))
+    assert np.abs(S).max() <= 1e-7
+    hp3 = rng.random(dim + 2)
+    hp3[-1] = 1e-5
+    mu3, S3 = O.predict([SE, WN], hp3, x, y, x)
+    assert np.linalg.norm(mu3 - y) <= 1e-3 * max(np.linalg.norm(mu3), np.linalg.norm(y))
+    assert np.abs(S3).max() <= 1e-3
+
+
 def test_interpolation_and_diag_vs_full():
-    """test/test_models.jl:17-48."""
+    """test/test_models.jl:34-48."""
     rng = np.random.default_rng(3)
     dim, n, npred = 2, 200, 100
     x, xp = rng.random((dim, n)), rng.random((dim, npred))
     y = np.sin(x.sum(0)) ** 2
-    hp = np.r_[1.0, [8.0] * dim, 0.8, [10.0] * dim]  # well-posed regime of the random-hp test
-    mu, S = O.predict([SE, SE], hp, x, y, x)
-    # Julia's `a ≈ b rtol=1e-7` on arrays is normwise; Sigma ≈ 0 checked elementwise
-    assert np.linalg.norm(mu - y) <= 1e-7 * np.linalg.norm(y)
-    assert np.abs(S).max() <= 1e-7
     hp = rng.random(dim + 2) + 0.5
     _, Sf = O.predict([SE, WN], hp, x, y, xp)
     _, Sd = O.predict([SE, WN], hp, x, y, xp, diagonal_var=True)

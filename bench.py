@@ -121,8 +121,8 @@ def parse():
     ap.add_argument("--kernel", default="SE+SE+WN")
     ap.add_argument("--nb", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-n", type=int, default=8192)
-    ap.add_argument("--cpu-np", type=int, default=2048)
+    ap.add_argument("--cpu-n", type=int, default=16384)
+    ap.add_argument("--cpu-np", type=int, default=4096)
     ap.add_argument("--no-split", action="store_true",
                     help="skip the C5 split-predict leg (extra key `split_predict`)")
     ap.add_argument("--split-steps", type=int, default=2)
@@ -144,10 +144,28 @@ def default_hp(kinds, d, noise=0.1):
     return np.array(hp, dtype=np.float64)
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(a, kinds, hp):
-    """Time the CPU oracle (test infrastructure, bench's cpu_baseline leg only) on a bounded
-    sample and scale each stage to the full job by its complexity."""
+    """Time the CPU oracle (test infrastructure, bench's cpu_baseline leg only): the reference's
+    call order (K-build, dpotrf, dpotrs, K(x, xp), mean, dtrsm, row norms) on a bounded sample
+    of the C3 job, N = a.cpu_n, np = a.cpu_np (default 16384 / 4096: the full N = 32768 job is
+    ~1 min per run on 16 host threads, and SciPy's OpenBLAS 0.3.28 dpotrf returns info = 16545
+    on the positive definite C3 matrix at N = 32768 -- see DESIGN.md), median of 3 runs after
+    one warm-up, each stage scaled to N = 32768, np = 8192 by its complexity (N^2, N^3, N^2,
+    np N^2).  Threads: the box's CPU share (OMP_NUM_THREADS, 16 on the GPU box) for both the
+    OpenMP K-build and OpenBLAS, set explicitly and reported as measured by threadpoolctl."""
     import scipy.linalg as sla
+    from threadpoolctl import threadpool_info, threadpool_limits
 
     from oracle import gpr_oracle as O
     from oracle.cpu_kbuild import kbuild_cpu
@@ -157,7 +175,7 @@ def cpu_baseline(a, kinds, hp):
     y = np.sin(x.sum(0)) ** 2
     xp = np.random.default_rng(1).random((d, m))
     okinds = [O.SE if k == 1 else O.WN for k in kinds]
-    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
 
     def run():
         t0 = time.perf_counter()
@@ -176,8 +194,13 @@ def cpu_baseline(a, kinds, hp):
         assert np.isfinite(mu).all() and np.isfinite(var).all()
         return np.array([t1 - t0, t2 - t1, t3 - t2, t4 - t3])
 
-    run()  # warm-up
-    reps = [run() for _ in range(3)]
+    with threadpool_limits(limits=threads):
+        blas = [{"lib": i.get("internal_api"), "version": i.get("version"),
+                 "threads": i.get("num_threads")}
+                for i in threadpool_info() if i.get("user_api") == "blas"
+                and "scipy.libs" in i.get("filepath", "")]  # SciPy's own OpenBLAS (LAPACK)
+        run()  # warm-up
+        reps = [run() for _ in range(3)]
     t = np.median(np.stack(reps), axis=0)
     N, NP = a.n, a.npred
     scale = np.array([(N / n) ** 2, (N / n) ** 3, (N / n) ** 2, (NP / m) * (N / n) ** 2])
@@ -187,10 +210,16 @@ def cpu_baseline(a, kinds, hp):
         "unit": "GP jobs/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"oracle (C OpenMP K-build + OpenBLAS dpotrf/dtrsm via SciPy) at N={n}, "
-                   f"np={m}, median of 3 after 1 warm-up: stages [kbuild, potrf, potrs, "
-                   f"posterior] = {[round(v, 4) for v in t.tolist()]} s, scaled to N={N}, "
-                   f"np={NP} by N^2 / N^3 / N^2 / np*N^2 -> {t_job:.2f} s per job"),
+        "cpu_model": _cpu_model(),
+        "blas": blas,
+        "measured_config": {"N": n, "np": m, "d": d, "kernel": a.kernel,
+                            "stage_s": [round(v, 4) for v in t.tolist()],
+                            "job_s": round(float(np.sum(t)), 4)},
+        "sample": (f"oracle (C OpenMP K-build + OpenBLAS dpotrf/dpotrs/dtrsm via SciPy, "
+                   f"{threads} threads) on the C3 job at N={n}, np={m} (median of 3 after 1 "
+                   f"warm-up): stages [kbuild, potrf, potrs, posterior] = "
+                   f"{[round(v, 4) for v in t.tolist()]} s; extrapolated to N={N}, np={NP} "
+                   f"by N^2 / N^3 / N^2 / np*N^2 -> {t_job:.2f} s per job"),
     }
 
 
@@ -232,9 +261,19 @@ def split_leg(a, world, rank, local):
     xe = np.random.default_rng(2).random((d, ne))
     xq = np.random.default_rng(3).random((d, nq))
     hp = np.r_[1.0, [3.0 * math.sqrt(8.0 / d)] * d, 0.1]
-    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=G.Context(local))
-    cm = G.Cmap("+", xe, xq)
+    err = None
+    try:
+        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=G.Context(local))
+        cm = G.Cmap("+", xe, xq)
+    except Exception as e:  # noqa: BLE001 -- every rank abandons the leg together
+        err = e
+    bad = torch.tensor([0 if err is None else 1], dtype=torch.int64,
+                       device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if int(bad.item()):
+        raise err if err is not None else RuntimeError("C5 leg: set-up failed on another rank")
     flops = 2.0 * ne * ns * nq + float(nq) * ns * ns * vr
+    coll = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
 
     def timed(fit):
         step = lambda: split_predict_distributed(md, cm, var_range=(1, vr), fit=fit)  # noqa: E731
@@ -247,7 +286,8 @@ def split_leg(a, world, rank, local):
         torch.cuda.synchronize()
         dist.barrier()
         dt = (time.perf_counter() - t0) / a.split_steps
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([dt], dtype=torch.float64,
+                          device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item()), bool(np.isfinite(mu).all() and np.isfinite(var).all())
 
@@ -256,8 +296,8 @@ def split_leg(a, world, rank, local):
            "unit": "test points/s (whole job)", "ms_per_step": dt * 1e3, "n_gpus": world,
            "steps": a.split_steps, "scaling": "strong",
            "workload": f"C5 split predict SE+WN ns={ns} d={d} ne={ne} nq={nq} var_rows={vr} "
-                       f"fit=broadcast, cost-balanced e-row shards x{world}, RCCL broadcast of "
-                       "U's packed upper triangle + all_gather",
+                       f"fit=broadcast, cost-balanced e-row shards x{world}, {coll} broadcast "
+                       "of U's packed upper triangle + all_gather",
            "algorithmic_TFLOPs": flops / dt / 1e12, "results_finite": ok}
     if world > 1:  # every rank refits instead of receiving U (no N^2 exchange)
         dt_r, ok_r = timed("replicate")
@@ -270,7 +310,13 @@ def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if a.dist_backend == "gloo":  # rehearsal: ranks share the devices there are
+        local %= max(ndev, 1)
+    elif local >= ndev:
+        sys.exit(f"bench.py: LOCAL_RANK={local} but only {ndev} HIP device(s) are visible "
+                 "(one rank per GPU under RCCL; --dist-backend gloo rehearses more ranks)")
     if world > 1:
         torch.cuda.set_device(local)
         with _StdoutToStderr():
@@ -440,7 +486,12 @@ def main():
                 "pmc_mfma": pmc_mfma(dominant[0], N, NP),
             },
             "results_finite": ok,
+            "dist_backend": a.dist_backend if world > 1 else None,
+            "physical_gpus": ndev,
         }
+        if world > 1 and a.dist_backend == "gloo":
+            out["rehearsal"] = (f"{world} ranks sharing {ndev} device(s) over gloo: plumbing "
+                                "check, not scaling data")
     split = None
     if not a.no_split:
         try:
@@ -452,6 +503,8 @@ def main():
                                             device_id=torch.device("cuda", local))
                 split = split_leg(a, dist.get_world_size(), rank, local)
         except Exception as ex:  # never let the C5 leg kill the headline line
+            # (split_predict_distributed exchanges a status before each data collective, so a
+            # failure raises on every rank at the same point and no rank is left blocked)
             split = {"value": None, "error": repr(ex)}
     if rank == 0:
         out["split_predict"] = split

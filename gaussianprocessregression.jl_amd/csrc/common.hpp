@@ -80,6 +80,9 @@ struct gpr_ctx {
   // 32768 193 -> 173.4 (67.7 TF/s); C3 fit + predict in one DAG launch 321.8 -> 305.5 ms.
   int dag_mode = 1;
   int dag_nmin = 0, dag_nmax = 1 << 30;
+  long long dag_spin_limit = 1ll << 25;  // DAG dependency wait bound in polls (~4 s); the
+                                        // GPR_DAG_SPIN_LIMIT environment variable overrides
+                                        // it per launch (tests force timeouts with it)
   int dag_zlag = 2;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
   int dag_rlag = 0;       // other right-hand-side rows after A's row i + lag (GPR_DAG_RLAG;
                           // 1, 2, 4 measured no faster for C2 / C3)

@@ -110,6 +110,7 @@ struct DagArgs {
   double* G;     // optional (lower B only): G += B^T B, upper tiles (i <= j), ld ldg --
   size_t ldg;    // K^{-1} = Z^T Z; tickets >= gbase are these tiles
   int gbase;
+  long long spin_limit;  // polls before a wait gives up (~4 s at 2^25; GPR_DAG_SPIN_LIMIT, tests)
 };
 
 __device__ __forceinline__ int ld_sc1(const int* p) {
@@ -265,14 +266,14 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
 // returns min(pa, pb, cap), uniform across the workgroup.  Bounded: after ~2^25 polls the
 // launch is flagged (info = -1) and the wait returns cap (results are garbage, the grid drains).
 __device__ __forceinline__ int dag_wait(const int* pa, const int* pb, int have, int cap,
-                                        int* info, int* sh) {
+                                        int* info, long long limit, int* sh) {
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
     int v = 0;
     long long spins = 0;
     for (;;) {
       v = __builtin_amdgcn_readfirstlane(min(ld_sc1(pa), ld_sc1(pb)));
       if (v > have) break;
-      if (++spins > (1ll << 25)) {
+      if (++spins > limit) {
         atomicCAS(info, 0, -1);
         v = cap;
         break;
@@ -331,7 +332,7 @@ __device__ __forceinline__ void dag_gram_task(const DagArgs& a, int i_, int j_,
   const double* Qcol = a.B + (size_t)j * DT * a.ldb;
   int done = j;
   while (done < nt) {
-    const int r = dag_wait(rhsprog + i, rhsprog + j, done, nt, a.info, s_wait);
+    const int r = dag_wait(rhsprog + i, rhsprog + j, done, nt, a.info, a.spin_limit, s_wait);
     const int nst = (min(r * DT, n) - done * DT) / DTK;  // (the last block may be short)
     dag_accum(acc, Pcol + (size_t)done * DT, a.ldb, mv, Qcol + (size_t)done * DT, a.ldb, nv, nst,
               lds);
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
       int done = (rhs && a.lower) ? j : 0;
       while (done < i) {
         int r = 0;
-        PROF(p_wait, r = dag_wait(colprog + i, pj, done, i, a.info, &s_wait));
+        PROF(p_wait, r = dag_wait(colprog + i, pj, done, i, a.info, a.spin_limit, &s_wait));
         PROF(p_acc, dag_accum(acc, Pcol + (size_t)done * DT, a.lda, mv, Qcol + (size_t)done * DT,
                               ldt, nv, (r - done) * (DT / DTK), lds));
         done = r;
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        PROF(p_wait, dag_wait(colprog + i, colprog + i, i, i + 1, a.info, &s_wait));  // W_i final
+        PROF(p_wait, dag_wait(colprog + i, colprog + i, i, i + 1, a.info, a.spin_limit, &s_wait));  // W_i final
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -719,6 +720,9 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   a.G = gram ? dG : nullptr;
   a.ldg = (size_t)(gram ? ldg : 0);
   a.gbase = gram ? ctx->dag_ntasks - nt * (nt + 1) / 2 : ctx->dag_ntasks;
+  // (re-read per launch: the timeout tests shorten it around one call)
+  const char* sl = getenv("GPR_DAG_SPIN_LIMIT");
+  a.spin_limit = sl ? std::max(1ll, atoll(sl)) : ctx->dag_spin_limit;
   const int grid = std::min(ctx->dag_ntasks, ctx->ncu);
   // factorisation n^3/3; U^{-T} B: n^2 per column, ~n^3/3 for a lower-triangular n x n B
   const double flops = (solve ? 0.0 : (double)n * n * n / 3.0) +

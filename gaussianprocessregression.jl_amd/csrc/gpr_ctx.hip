@@ -315,6 +315,14 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2) {
   return 0;
 }
 
+int gpr_forget_factor(gpr_ctx_t ctx) {
+  ctx->fac_valid = false;
+  ctx->fac_ptr = nullptr;
+  ctx->sqinv_nb2 = 0;
+  ctx->sq_ptr = nullptr;
+  return 0;
+}
+
 int gpr_timing_enable(gpr_ctx_t ctx, int on) {
   ctx->timing = on != 0;
   return 0;

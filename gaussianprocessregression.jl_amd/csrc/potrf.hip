@@ -1970,10 +1970,20 @@ int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int
     // the tile-DAG with every tile of U final: only B's tiles are tasks (left-looking, one
     // long-K accumulation per tile, W_i from the factor's block inverses)
     GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
+    // the kernel skips every task while info != 0: clear what an earlier launch left, and
+    // read it back afterwards (a timed-out dependency wait leaves B unsolved: report it)
+    HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), ctx->stream));
     const int rc = launch_potrf_dag(ctx, const_cast<double*>(dU), n, ldu, dB, nrhs, ldb, 0,
                                     ctx->stream, DAG_SOLVE | (lower_rhs ? DAG_LOWER : 0));
     if (rc < 0) return rc;
     if (rc == 0) {
+      int hinfo = 0;
+      HIP_TRY(ctx, hipMemcpyAsync(&hinfo, ctx->dinfo, sizeof(int), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      if (hinfo != 0)
+        return set_err(ctx, GPR_E_HIP, "tile-DAG solve: a dependency wait timed out (info %d)",
+                       hinfo);
       if (norm_out) GPR_TRY(launch_colnorm_sub(ctx, dB, ldb, n, nrhs, norm_out));
       return 0;
     }

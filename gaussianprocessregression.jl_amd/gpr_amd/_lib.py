@@ -57,6 +57,7 @@ _SIGS = {
     "gpr_timing_enable": (_i, [_p, _i]),
     "gpr_timing_get": (_i, [_p, _i, _dp, POINTER(c_longlong), _dp]),
     "gpr_timing_reset": (_i, [_p]),
+    "gpr_forget_factor": (_i, [_p]),
     "gpr_kernel": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _d, _p, _i]),
     "gpr_kernel_grad": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _i, _d, _p, _i]),
     "gpr_potrf_upper": (_i, [_p, _p, _i, _i, _ip]),

@@ -124,6 +124,9 @@ class HipSplitBackend:
 
     def receive(self):
         self.ctx.stream.wait_stream(torch.cuda.current_stream(self.device))
+        # the broadcast wrote U behind the context's back: a cached factor keyed on the same
+        # device pointer (a re-used allocation) must not serve this one
+        self.ctx.check(lib.gpr_forget_factor(self.ctx.h), "gpr_forget_factor")
 
     def predict_rows(self, cm: core.Cmap, U, wt, e_lo: int, e_hi: int, v_lo: int, v_hi: int):
         md, ctx = self.md, self.ctx
@@ -253,14 +256,26 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
     emax = max(max(rows), 1)
     mu_sh = var_sh = None
     off = 0
-    for lo, hi in pieces[rank]:
-        mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
-        if mu_sh is None:
-            mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
-            var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
-        mu_sh[:, off:off + hi - lo] = mu_full[:, lo:hi]
-        var_sh[off * nq:(off + hi - lo) * nq] = var_full[lo * nq:hi * nq]
-        off += hi - lo
+    err = None
+    try:
+        for lo, hi in pieces[rank]:
+            mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+            if mu_sh is None:
+                mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
+                var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
+            mu_sh[:, off:off + hi - lo] = mu_full[:, lo:hi]
+            var_sh[off * nq:(off + hi - lo) * nq] = var_full[lo * nq:hi * nq]
+            off += hi - lo
+    except Exception as e:  # noqa: BLE001 -- re-raised after the status exchange
+        err = e
+    # as for the fit: every rank learns of a failed shard before the all_gather, so all ranks
+    # raise instead of the healthy ones blocking in the collective
+    bad = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=group)
+    if int(bad.item()):
+        if err is not None:
+            raise err
+        raise GprError("split_predict_distributed: a shard failed on another rank")
     if mu_sh is None:  # no rows here (more ranks than rows)
         mu_sh = torch.zeros(nq, emax, dtype=torch.float64, device=dev)
         var_sh = torch.zeros(emax * nq, dtype=torch.float64, device=dev)

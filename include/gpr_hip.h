@@ -123,6 +123,13 @@ int gpr_kernel_grad(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
  * GPR_DAG=0 in the environment selects the blocked two-stream factorisation. */
 int gpr_potrf_upper(gpr_ctx_t ctx, double* dA, int n, int lda, int* info);
 
+/* The context caches the factor's block inverses (and the outer squares' inverses) after a
+ * factorisation or a first solve, keyed on the factor's device pointer and shape.  A factor
+ * written into a buffer by anything other than this context (a broadcast, a copy, another
+ * context) must be announced with gpr_forget_factor, or a following solve on the same pointer
+ * reuses inverses of the previous contents. */
+int gpr_forget_factor(gpr_ctx_t ctx);
+
 /* B <- K^{-1} B for K = U^T U (dU from gpr_potrf_upper), B n x nrhs (ldb).
  * Replaces ldiv!(alpha, kchol, y) = dpotrs (src/cost.jl:79,89,106, src/predict.jl:32). */
 int gpr_potrs_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dB, int nrhs,

@@ -43,3 +43,33 @@ def kbuild_cpu(kinds, hp, x, xp=None, eps=O.EPS_DEFAULT) -> np.ndarray:
                    1 if (wn and xp is None) else 0, float(wn[0][0] ** 2) if wn else 0.0, eps,
                    P(K))
     return K.T
+
+
+def fit_upper_inplace(kinds, hp, x, y, eps=O.EPS_DEFAULT, backend="scipy"):
+    """update_cache!(pc, md) (src/predict.jl:29-34) at sizes where the NumPy restatement's
+    temporaries do not fit in host memory (N = 32768: K alone is 8.6 GB): K by the threaded C
+    restatement above, dpotrf('U') in place on it (LAPACK, like cholesky!(Hermitian(K)) --
+    the strict lower triangle keeps K), wt = K^{-1} y by the oracle's own cho_solve_upper.
+    Returns (U buffer, wt).  tests/test_oracle.py checks it against O.chol_upper /
+    O.cho_solve_upper at small N.
+
+    backend "scipy": LAPACK dpotrf of SciPy's bundled OpenBLAS.  backend "mkl": the
+    dpotrf of torch's CPU build (MKL LAPACK; torch is host plumbing here).  SciPy's
+    scipy-openblas 0.3.28 returns info = 16545 for the positive definite C3 matrix
+    (SE+SE+WN, N = 32768; N = 24576 factors fine), so the full-size fixtures use "mkl" and
+    verify every result by residuals (tests/golden/make_fullsize.py)."""
+    import scipy.linalg as sla
+
+    K = kbuild_cpu(kinds, hp, x, None, eps)         # Fortran-ordered n x n
+    if backend == "mkl":
+        import torch
+
+        U, info = torch.linalg.cholesky_ex(torch.from_numpy(K.T), upper=True)  # K symmetric
+        info = int(info)
+        U = U.numpy()  # row-major: U[i, j] = U_ij, strict lower triangle zero
+        del K
+    else:
+        U, info = sla.lapack.dpotrf(K, lower=0, clean=0, overwrite_a=1)
+    if info != 0:
+        raise np.linalg.LinAlgError(f"dpotrf info={info}")
+    return U, O.cho_solve_upper(U, y)

@@ -210,6 +210,15 @@ def mll(kinds, hp, x, y, eps=EPS_DEFAULT, train_axis=1):
     return mll_value(U, ys, alpha)
 
 
+def mll_grad_parts(dK, alpha: np.ndarray, Kinv: np.ndarray) -> Tuple[float, float]:
+    """The two terms of grad(MLL, kchol, dK, alpha, K^-1, tt) src/loss_grad.jl:43-52:
+    (alpha' dK alpha, <K^-1, dK>_F); the component is -0.5 (first - second)."""
+    if isinstance(dK, tuple):  # UniformScaling lam*I: src/loss_grad.jl:50-52
+        return dK[1] * float(np.sum(alpha ** 2)), dK[1] * float(np.sum(np.diag(Kinv)))
+    tt = dK @ alpha
+    return float(np.dot(tt, alpha)), float(np.sum(Kinv * dK))
+
+
 def mll_grad_term(dK, alpha: np.ndarray, Kinv: np.ndarray) -> float:
     """grad(MLL, kchol, dK, alpha, K^-1, tt) src/loss_grad.jl:43-52."""
     if isinstance(dK, tuple):  # UniformScaling
@@ -260,10 +269,17 @@ def predict(kinds, hp, x, y, xp, diagonal_var=False, eps=EPS_DEFAULT):
 
     Returns (mu, Sigma) with Sigma an np x np matrix (full) or the np diagonal vector.
     """
-    d = x.shape[0]
     K = kernel(kinds, hp, x, None, eps)
     U = chol_upper(K)
     wt = cho_solve_upper(U, y)                    # ldiv!(pc.wt, kchol, md.y)
+    return predict_from_factor(kinds, hp, x, U, wt, xp, diagonal_var, eps)
+
+
+def predict_from_factor(kinds, hp, x, U, wt, xp, diagonal_var=False, eps=EPS_DEFAULT):
+    """predict!(mu, Sigma, md, xp, pc) src/predict.jl:36-71 from an updated cache: U is the
+    upper factor (only its upper triangle is read, like Cholesky(UpperTriangular(pc.Kxx))),
+    wt = K^{-1} md.y."""
+    d = x.shape[0]
     Kxp = kernel(kinds, hp, xp, x, eps)           # np x N; eps per SE part iff xp is x
     mu = Kxp @ wt
     V = sla.solve_triangular(U, Kxp.T, trans="T", lower=False, check_finite=False).T  # rdiv!(Kxp,U)
@@ -330,17 +346,26 @@ def split_predict(kinds, hp, x, y, xe, xq, var_range: Tuple[int, int] | None = (
     variance diagonal of length ne*nq whose entry (e-1)*nq + q is updated only for
     e in var_range (1-based inclusive); every other entry keeps the prior.
     """
-    d = x.shape[0]
-    ne, nq = xe.shape[1], xq.shape[1]
     K = kernel(kinds, hp, x, None, eps)
     U = chol_upper(K)
     wt = cho_solve_upper(U, y)
+    return split_predict_from_factor(kinds, hp, x, U, wt, xe, xq, var_range, eps)
+
+
+def split_predict_from_factor(kinds, hp, x, U, wt, xe, xq, var_range=(1, 3), eps=EPS_DEFAULT,
+                              mean_rows=None):
+    """The split predict! (src/split_predict.jl:5-53) from an updated cache (U upper factor,
+    wt = K^{-1} y).  ``mean_rows`` (0-based e indices) restricts the returned mean to those
+    grid rows (a row of mu needs only its own row of A and B)."""
+    d = x.shape[0]
+    ne, nq = xe.shape[1], xq.shape[1]
     A, B, C = split_factors(kinds, hp, x, xe, xq, eps)
-    mu = np.zeros((ne, nq))
+    rows = np.arange(ne) if mean_rows is None else np.asarray(mean_rows)
+    mu = np.zeros((len(rows), nq))
     for k in range(A.shape[2]):
         Cw = wt[:, None] * C[:, :, k]
-        BCw = B[:, :, k] @ Cw
-        mu += BCw * A[:, :, k]
+        BCw = B[rows, :, k] @ Cw
+        mu += BCw * A[rows, :, k]
     var = np.full(ne * nq, diag_prior(kinds, hp, d))
     if var_range is not None:
         lo, hi = var_range

@@ -124,9 +124,14 @@ def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit)
 class FailingBackend(OracleBackend):
     """fit() raises on the ranks listed in `fail` (PosDefException(info) or a generic error)."""
 
-    def __init__(self, *a, fail=(), info=7, **kw):
+    def __init__(self, *a, fail=(), info=7, fail_rows=(), **kw):
         super().__init__(*a, **kw)
-        self.fail, self.info = fail, info
+        self.fail, self.info, self.fail_rows = fail, info, fail_rows
+
+    def predict_rows(self, *a, **kw):
+        if dist.get_rank() in self.fail_rows:
+            raise RuntimeError("simulated shard failure")
+        return super().predict_rows(*a, **kw)
 
     def fit(self):
         if dist.get_rank() in self.fail:
@@ -137,12 +142,12 @@ class FailingBackend(OracleBackend):
         return super().fit()
 
 
-def _fail_worker(rank, world, port, out, fit, fail, info):
+def _fail_worker(rank, world, port, out, fit, fail, info, fail_rows=()):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         kinds, hp, x, y, xe, xq = _problem(ne=5, nq=3)
-        be = FailingBackend(kinds, hp, x, y, fail=fail, info=info)
+        be = FailingBackend(kinds, hp, x, y, fail=fail, info=info, fail_rows=fail_rows)
         try:
             gd.split_predict_distributed(None, _Cmap(xe, xq), backend=be, fit=fit)
             res = "ok"
@@ -249,6 +254,14 @@ def test_split_predict_distributed_hip_single_rank():
         dist.destroy_process_group()
 
 
+def _hp_iter(hp, it):
+    hp = np.array(hp, dtype=np.float64)
+    if it == 1:
+        hp[1:-1] *= 1.3
+        hp[-1] *= 0.7
+    return hp
+
+
 def _hip_gloo_worker(rank, world, port, out, fit):
     """Two ranks on ONE GPU over gloo with device tensors: the HIP backend's stream ordering
     around the collectives (gpr_fit leaves the wt solve queued on the context stream; the
@@ -258,9 +271,11 @@ def _hip_gloo_worker(rank, world, port, out, fit):
     try:
         import gpr_amd as G
         kinds, hp, x, y, xe, xq = _problem(ne=9, nq=40, ns=4096, d=6, seed=11)
-        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
         cm = G.Cmap("+", xe, xq)
         for it in range(3):
+            # iteration 1 changes the hyperparameters: a rank that receives U into a re-used
+            # allocation must not solve with the previous factor's cached inverses
+            md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), _hp_iter(hp, it), x, y)
             mu, var = gd.split_predict_distributed(md, cm, var_range=(1, 9), fit=fit)
             np.save(os.path.join(out, f"mu{rank}_{it}.npy"), mu)
             np.save(os.path.join(out, f"var{rank}_{it}.npy"), var)
@@ -277,9 +292,21 @@ def test_split_predict_distributed_hip_two_ranks(tmp_path, fit):
     G = pytest.importorskip("gpr_amd")
     mp.spawn(_hip_gloo_worker, args=(2, _free_port(), str(tmp_path), fit), nprocs=2, join=True)
     kinds, hp, x, y, xe, xq = _problem(ne=9, nq=40, ns=4096, d=6, seed=11)
-    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
-    mu1, var1 = G.predict(md, G.Cmap("+", xe, xq), diagonal_var=True, var_range=(1, 9))
-    for r in range(2):
-        for it in range(3):
+    for it in range(3):
+        md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), _hp_iter(hp, it), x, y)
+        mu1, var1 = G.predict(md, G.Cmap("+", xe, xq), diagonal_var=True, var_range=(1, 9))
+        for r in range(2):
             np.testing.assert_allclose(np.load(tmp_path / f"mu{r}_{it}.npy"), mu1, rtol=1e-12, atol=1e-14)
             np.testing.assert_allclose(np.load(tmp_path / f"var{r}_{it}.npy"), var1, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("fit", ["broadcast", "replicate"])
+def test_split_predict_distributed_shard_failure(tmp_path, fit):
+    """A shard that fails on one rank (rank 1's predict_rows raises) raises on EVERY rank
+    instead of leaving the others blocked in the all_gather."""
+    world = 3
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path), fit, (), 0, (1,)),
+             nprocs=world, join=True)
+    res = [open(tmp_path / f"r{r}.txt").read() for r in range(world)]
+    assert res[1].startswith("RuntimeError"), res
+    assert res[0].startswith("GprError") and res[2].startswith("GprError"), res

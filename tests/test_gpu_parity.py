@@ -495,6 +495,44 @@ def test_potri_and_trsm(n, dag_solve, monkeypatch):
         assert relnorm(ctx.host(dB), sla.solve_triangular(U, B, trans="T")) < 1e-11
 
 
+def test_dag_wait_timeout_drains_and_context_recovers(monkeypatch):
+    """Every tile-DAG dependency wait is bounded (dag.hip dag_wait); GPR_DAG_SPIN_LIMIT=1
+    forces the bound to expire.  The launch must drain (no hang), the call must return
+    GPR_E_HIP with the timeout message -- the factorisation (gpr_fit_predict) and a solve-only
+    launch (gpr_potri_upper's Z) alike -- and the SAME context must give correct results once
+    the bound is back: the info flag a timed-out launch leaves behind must not make the next
+    solve-only launch skip its tasks."""
+    monkeypatch.setenv("GPR_DAG_SOLVE", "1")   # the solve-only tile-DAG at this size
+    ctx = G.Context(0)
+    n = 1024
+    A = _spd(n, seed=3)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    dK = ctx.empty(n, n)
+    potri = lambda: G._lib.lib.gpr_potri_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,  # noqa: E731
+                                               ctypes.c_void_p(dK.data_ptr()), n)
+    x, y, xp = O.synthetic(4, 1024, 200, seed_train=5)
+    kinds = [SE, WN]
+    hp = O.default_hp(kinds, 4)
+    md = G.GPRModel(cov_of(kinds), hp, x, y, ctx=ctx)
+    monkeypatch.setenv("GPR_DAG_SPIN_LIMIT", "1")
+    for _ in range(2):  # (twice: a drained launch leaves the context usable for the next one)
+        with pytest.raises(G.GprError, match="timed out"):
+            G.predict(md, xp, diagonal_var=True)
+        assert potri() == -2
+        assert b"timed out" in G._lib.lib.gpr_last_error(ctx.h)
+    monkeypatch.delenv("GPR_DAG_SPIN_LIMIT")
+    # the factor in dA is intact (the timed-out launches were solves / other buffers); the
+    # solve-only launch right after a timed-out one on the same cached factor (its block
+    # inverses are a cache hit, so nothing else clears the info flag in between)
+    assert potri() == 0
+    assert relnorm(ctx.host(dK), np.linalg.inv(A)) < 1e-11
+    mu, var = G.predict(md, xp, diagonal_var=True)
+    mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+    np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-8 * O.diag_prior(kinds, hp, 4))
+
+
 # ---------------------------------------------------------------------------------------
 # a8/a9 MLL value and gradient  (test/test_loss.jl)
 # ---------------------------------------------------------------------------------------

@@ -225,3 +225,20 @@ def test_mpmath_bounds_oracle_error():
     alpha = O.cho_solve_upper(U, y)
     np.testing.assert_allclose(alpha, np.array([float(v) for v in amp]), rtol=1e-11)
     assert O.mll_value(U, y, alpha) == pytest.approx(float(mll_mp), rel=1e-13)
+
+
+def test_fit_upper_inplace_matches_oracle():
+    """oracle/cpu_kbuild.fit_upper_inplace (the lean fit behind the full-size fixtures,
+    tests/golden/make_fullsize.py) against the NumPy restatement."""
+    from oracle.cpu_kbuild import fit_upper_inplace
+    for kinds, backend in (([SE], "scipy"), ([SE, SE, WN], "scipy"), ([SE, SE, WN], "mkl")):
+        x, y, xp = O.synthetic(8, 512, 64)
+        hp = O.default_hp(kinds, 8)
+        U, wt = fit_upper_inplace(kinds, hp, x, y, backend=backend)
+        U_o = O.chol_upper(O.kernel(kinds, hp, x))
+        np.testing.assert_allclose(np.triu(U), U_o, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(wt, O.cho_solve_upper(U_o, y), rtol=1e-10)
+        mu, var = O.predict_from_factor(kinds, hp, x, U, wt, xp, diagonal_var=True)
+        mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+        np.testing.assert_allclose(mu, mu_o, rtol=1e-12)
+        np.testing.assert_allclose(var, var_o, rtol=1e-10, atol=1e-14)

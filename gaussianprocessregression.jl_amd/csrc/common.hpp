@@ -163,6 +163,12 @@ struct gpr_ctx {
 };
 
 // ---- error helpers -------------------------------------------------------------------
+// split prediction of sorted, disjoint row pieces [pieces[2k], pieces[2k+1]) (predict.hip)
+int split_predict_pieces(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d,
+                         const double* dX, int ns, const double* dU, int ldu, const double* dwt,
+                         const double* dXe, int ne, const double* dXq, int nq, const int* pieces,
+                         int npieces, int var_lo, int var_hi, double eps, double* dmu,
+                         double* dvar);
 int set_err(gpr_ctx* ctx, int code, const char* fmt, ...);
 
 #define HIP_TRY(ctx, expr)                                                          \

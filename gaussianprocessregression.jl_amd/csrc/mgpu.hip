@@ -1,0 +1,380 @@
+// mgpu.hip -- split-kernel block prediction sharded over the GPUs of one node, in ONE host
+// process (src/split_predict.jl:5-53 is the single-CPU reference).
+//
+// The grid rows e of x_{e,q} = xe_e + xq_q are independent once the training factor U and the
+// weights wt = K^{-1} y exist:
+//   1. fit  -- GPR_MGPU_BROADCAST: device 0 fits (K, tile-DAG POTRF, wt) and RCCL broadcasts
+//              U's upper triangle packed by 128-column blocks (~4 N^2 bytes instead of 8 N^2)
+//              plus wt over xGMI; the receivers unpack it into their U and drop their cached
+//              block inverses (rebuilt from the received factor).
+//              GPR_MGPU_REPLICATE: every device fits for itself (no N^2 exchange: the fit is
+//              ~180 ms at ns = 32768 while the packed broadcast moves 4.3 GB).
+//   2. rows -- device i takes gpr_shard_pieces(ne, ngpu, i, var_lo, var_hi): an even share of
+//              the variance rows (an ns^2 triangular solve per test point) and of the mean-only
+//              rows, as at most three contiguous pieces, all in one split_predict_pieces call
+//              (the ns x nq C factor built once per device).
+//   3. out  -- every device copies its rows of mu (ne x nq column-major, index e + q ne) and of
+//              the variance diagonal (index e nq + q) straight into the caller's host arrays
+//              (each GPU over its own PCIe link; no gather through one device).
+// One host thread per device drives phases 1-3 (each with the device current); the broadcast
+// is one RCCL group over all devices from the calling thread.  RCCL is loaded with dlopen, so
+// libgpr_hip.so has no link-time dependency on it and a host process that already carries a
+// librccl.so.1 (torch) shares that one.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "common.hpp"
+
+namespace {
+
+struct RcclApi {
+  void* h = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+// the process's librccl if one is loaded already, else the system's
+bool load_rccl(RcclApi* r, std::string* err) {
+  if (r->h) return true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) {
+    *err = std::string("cannot load librccl.so.1: ") + dlerror();
+    return false;
+  }
+  r->CommInitAll = (decltype(r->CommInitAll))dlsym(h, "ncclCommInitAll");
+  r->CommDestroy = (decltype(r->CommDestroy))dlsym(h, "ncclCommDestroy");
+  r->Broadcast = (decltype(r->Broadcast))dlsym(h, "ncclBroadcast");
+  r->GroupStart = (decltype(r->GroupStart))dlsym(h, "ncclGroupStart");
+  r->GroupEnd = (decltype(r->GroupEnd))dlsym(h, "ncclGroupEnd");
+  r->GetErrorString = (decltype(r->GetErrorString))dlsym(h, "ncclGetErrorString");
+  if (!r->CommInitAll || !r->CommDestroy || !r->Broadcast || !r->GroupStart || !r->GroupEnd ||
+      !r->GetErrorString) {
+    *err = "librccl.so.1 lacks an ncclCommInitAll / ncclBroadcast / ncclGroup* symbol";
+    return false;
+  }
+  r->h = h;
+  return true;
+}
+
+constexpr int PACK_NB = 128;
+
+// packed upper triangle by 128-column blocks: block b = columns [128 b, j1) keeps rows [0, j1)
+// of each of its columns, j1 = min(128 (b + 1), n); every block before the last is full, so
+// block b starts at 128^2 b (b + 1) / 2
+__host__ __device__ inline size_t pack_base(int b) {
+  return (size_t)PACK_NB * PACK_NB * (size_t)b * (size_t)(b + 1) / 2;
+}
+
+size_t packed_len(int n) {
+  const int nb = (n + PACK_NB - 1) / PACK_NB;
+  return nb ? pack_base(nb - 1) + (size_t)(n - (nb - 1) * PACK_NB) * n : 0;
+}
+
+// one workgroup row-strip per column c: rows [0, j1) of column c <-> packed, coalesced both ways
+template <bool PACK>
+__global__ __launch_bounds__(256) void pack_upper_kernel(double* __restrict__ U, size_t ldu, int n,
+                                                         double* __restrict__ P) {
+  const int c = blockIdx.x;
+  const int b = c / PACK_NB;
+  const int j1 = min((b + 1) * PACK_NB, n);
+  double* p = P + pack_base(b) + (size_t)(c - b * PACK_NB) * j1;
+  double* u = U + (size_t)c * ldu;
+  for (int r = blockIdx.y * 256 + threadIdx.x; r < j1; r += gridDim.y * 256) {
+    if (PACK)
+      p[r] = u[r];
+    else
+      u[r] = p[r];
+  }
+}
+
+int launch_pack(gpr_ctx* ctx, double* U, int ldu, int n, double* P, bool pack) {
+  if (n <= 0) return 0;
+  const dim3 grid(n, std::min(32, (n + 255) / 256));
+  if (pack)
+    pack_upper_kernel<true><<<grid, 256, 0, ctx->stream>>>(U, (size_t)ldu, n, P);
+  else
+    pack_upper_kernel<false><<<grid, 256, 0, ctx->stream>>>(U, (size_t)ldu, n, P);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+void shard_rows(int n, int world, int rank, int* lo, int* hi) {
+  const int q = n / world, r = n % world;
+  *lo = rank * q + std::min(rank, r);
+  *hi = *lo + q + (rank < r ? 1 : 0);
+}
+
+}  // namespace
+
+struct gpr_mgpu {
+  int ngpu = 0;
+  std::vector<int> dev;
+  std::vector<gpr_ctx_t> ctx;
+  std::vector<ncclComm_t> comm;
+  RcclApi rccl;
+  std::string err;
+  struct Bufs {  // device buffers of one GPU, grown on demand
+    double *x = nullptr, *y = nullptr, *xe = nullptr, *xq = nullptr, *U = nullptr, *wt = nullptr,
+           *mu = nullptr, *var = nullptr, *pk = nullptr;
+    size_t cx = 0, cy = 0, cxe = 0, cxq = 0, cU = 0, cwt = 0, cmu = 0, cvar = 0, cpk = 0;
+  };
+  std::vector<Bufs> buf;
+};
+
+namespace {
+
+int mg_err(gpr_mgpu* h, int code, const char* fmt, ...) {
+  char b[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(b, sizeof b, fmt, ap);
+  va_end(ap);
+  h->err = b;
+  return code;
+}
+
+// (called with the device current)
+bool grow(double** p, size_t* cap, size_t n) {
+  if (*cap >= n && *p) return true;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(double)) != hipSuccess) return false;
+  *cap = n;
+  return true;
+}
+
+// run f(i) for every device on its own host thread (device i current), collect return codes
+template <class F>
+std::vector<int> on_devices(gpr_mgpu* h, F f) {
+  std::vector<int> rc(h->ngpu, 0);
+  std::vector<std::thread> th;
+  for (int i = 0; i < h->ngpu; ++i)
+    th.emplace_back([&, i] {
+      if (hipSetDevice(h->dev[i]) != hipSuccess) {
+        rc[i] = GPR_E_HIP;
+        return;
+      }
+      rc[i] = f(i);
+    });
+  for (auto& t : th) t.join();
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpr_shard_pieces(int n, int world, int rank, int v_lo, int v_hi, int* pieces) {
+  if (n < 0 || world <= 0 || rank < 0 || rank >= world || !pieces) return GPR_E_ARG;
+  v_lo = std::max(0, std::min(v_lo, n));
+  v_hi = std::max(0, std::min(v_hi, n));
+  const int nv = std::max(v_hi - v_lo, 0);
+  int raw[6], np = 0, a, b;
+  if (nv) {
+    shard_rows(nv, world, rank, &a, &b);
+    if (b > a) {
+      raw[2 * np] = v_lo + a;
+      raw[2 * np + 1] = v_lo + b;
+      ++np;
+    }
+  }
+  shard_rows(n - nv, world, rank, &a, &b);  // mean-only index i < v_lo is row i, else i + nv
+  if (a < std::min(b, v_lo)) {
+    raw[2 * np] = a;
+    raw[2 * np + 1] = std::min(b, v_lo);
+    ++np;
+  }
+  const int lo2 = std::max(a, v_lo), hi2 = b;
+  if (hi2 > lo2) {
+    raw[2 * np] = lo2 + nv;
+    raw[2 * np + 1] = hi2 + nv;
+    ++np;
+  }
+  // sort by start, merge adjacent pieces
+  for (int i = 1; i < np; ++i)
+    for (int j = i; j > 0 && raw[2 * j] < raw[2 * (j - 1)]; --j) {
+      std::swap(raw[2 * j], raw[2 * (j - 1)]);
+      std::swap(raw[2 * j + 1], raw[2 * (j - 1) + 1]);
+    }
+  int m = 0;
+  for (int i = 0; i < np; ++i) {
+    if (m && pieces[2 * m - 1] == raw[2 * i]) {
+      pieces[2 * m - 1] = raw[2 * i + 1];
+    } else {
+      pieces[2 * m] = raw[2 * i];
+      pieces[2 * m + 1] = raw[2 * i + 1];
+      ++m;
+    }
+  }
+  return m;
+}
+
+int gpr_pack_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dP) {
+  if (n < 0 || ldu < std::max(n, 1) || (n && (!dU || !dP))) return set_err(ctx, GPR_E_ARG, "bad args");
+  return launch_pack(ctx, const_cast<double*>(dU), ldu, n, dP, true);
+}
+
+int gpr_unpack_upper(gpr_ctx_t ctx, const double* dP, int n, double* dU, int ldu) {
+  if (n < 0 || ldu < std::max(n, 1) || (n && (!dU || !dP))) return set_err(ctx, GPR_E_ARG, "bad args");
+  return launch_pack(ctx, dU, ldu, n, const_cast<double*>(dP), false);
+}
+
+size_t gpr_packed_upper_len(int n) { return n > 0 ? packed_len(n) : 0; }
+
+int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out) {
+  if (!out || ngpu <= 0 || !devices) return GPR_E_ARG;
+  *out = nullptr;
+  gpr_mgpu* h = new gpr_mgpu();
+  h->ngpu = ngpu;
+  h->dev.assign(devices, devices + ngpu);
+  h->ctx.assign(ngpu, nullptr);
+  h->buf.resize(ngpu);
+  for (int i = 0; i < ngpu; ++i) {
+    for (int j = 0; j < i; ++j)
+      if (h->dev[j] == h->dev[i]) {
+        gpr_mgpu_destroy(h);
+        return GPR_E_ARG;  // one rank per GPU (RCCL refuses two on one device)
+      }
+    if (gpr_ctx_create(h->dev[i], nullptr, &h->ctx[i]) != 0) {
+      gpr_mgpu_destroy(h);
+      return GPR_E_HIP;
+    }
+  }
+  std::string err;
+  if (!load_rccl(&h->rccl, &err)) {
+    gpr_mgpu_destroy(h);
+    return GPR_E_UNSUP;
+  }
+  h->comm.assign(ngpu, nullptr);
+  if (h->rccl.CommInitAll(h->comm.data(), ngpu, h->dev.data()) != ncclSuccess) {
+    h->comm.clear();
+    gpr_mgpu_destroy(h);
+    return GPR_E_HIP;
+  }
+  *out = h;
+  return 0;
+}
+
+int gpr_mgpu_destroy(gpr_mgpu_t h) {
+  if (!h) return 0;
+  for (int i = 0; i < h->ngpu; ++i) {
+    if (hipSetDevice(h->dev[i]) != hipSuccess) continue;
+    if (i < (int)h->comm.size() && h->comm[i] && h->rccl.CommDestroy) h->rccl.CommDestroy(h->comm[i]);
+    auto& b = h->buf[i];
+    for (double* p : {b.x, b.y, b.xe, b.xq, b.U, b.wt, b.mu, b.var, b.pk})
+      if (p) hipFree(p);
+    if (h->ctx[i]) gpr_ctx_destroy(h->ctx[i]);
+  }
+  delete h;
+  return 0;
+}
+
+const char* gpr_mgpu_last_error(gpr_mgpu_t h) { return h ? h->err.c_str() : "null handle"; }
+
+int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double* hp, int d,
+                           const double* X, int ns, const double* y, const double* Xe, int ne,
+                           const double* Xq, int nq, int var_lo, int var_hi, double eps,
+                           int fit_mode, double* mu, double* var, int* info) {
+  if (!h) return GPR_E_ARG;
+  if (info) *info = 0;
+  if (ns <= 0 || ne <= 0 || nq <= 0 || d <= 0 || !X || !y || !Xe || !Xq || !mu || !var || !kinds ||
+      !hp)
+    return mg_err(h, GPR_E_ARG, "bad args");
+  if (fit_mode != GPR_MGPU_BROADCAST && fit_mode != GPR_MGPU_REPLICATE)
+    return mg_err(h, GPR_E_ARG, "fit_mode %d is neither GPR_MGPU_BROADCAST nor _REPLICATE", fit_mode);
+  const int G = h->ngpu;
+  const bool bcast = fit_mode == GPR_MGPU_BROADCAST && G > 1;
+  const size_t npk = packed_len(ns);
+  std::vector<int> finfo(G, 0);
+  // 1. inputs up, fit (device 0, or every device), device 0 packs U for the broadcast
+  auto rc = on_devices(h, [&](int i) -> int {
+    gpr_ctx_t c = h->ctx[i];
+    auto& b = h->buf[i];
+    if (!grow(&b.x, &b.cx, (size_t)d * ns) || !grow(&b.y, &b.cy, ns) ||
+        !grow(&b.xe, &b.cxe, (size_t)d * ne) || !grow(&b.xq, &b.cxq, (size_t)d * nq) ||
+        !grow(&b.U, &b.cU, (size_t)ns * ns) || !grow(&b.wt, &b.cwt, ns) ||
+        !grow(&b.mu, &b.cmu, (size_t)ne * nq) || !grow(&b.var, &b.cvar, (size_t)ne * nq) ||
+        (bcast && !grow(&b.pk, &b.cpk, npk)))
+      return set_err(c, GPR_E_NOMEM, "device %d: allocation failed", h->dev[i]);
+    GPR_TRY(gpr_upload(c, b.x, X, sizeof(double) * d * ns));
+    GPR_TRY(gpr_upload(c, b.y, y, sizeof(double) * ns));
+    GPR_TRY(gpr_upload(c, b.xe, Xe, sizeof(double) * d * ne));
+    GPR_TRY(gpr_upload(c, b.xq, Xq, sizeof(double) * d * nq));
+    if (!bcast || i == 0) {
+      const int r = gpr_fit(c, kinds, nk, hp, d, b.x, ns, b.y, 1, ns, eps, b.U, ns, b.wt, &finfo[i]);
+      if (r != 0) return r;  // (> 0: the LAPACK info)
+      if (bcast) GPR_TRY(launch_pack(c, b.U, ns, ns, b.pk, true));
+    }
+    return gpr_sync(c);
+  });
+  for (int i = 0; i < G; ++i) {
+    if (finfo[i] > 0) {
+      if (info) *info = finfo[i];
+      return mg_err(h, finfo[i], "device %d: K is not positive definite (info %d)", h->dev[i],
+                    finfo[i]);
+    }
+    if (rc[i] < 0)
+      return mg_err(h, rc[i], "device %d: %s", h->dev[i], gpr_last_error(h->ctx[i]));
+  }
+  // 2. broadcast the packed factor and wt from device 0 (one RCCL group over all devices)
+  if (bcast) {
+    auto& R = h->rccl;
+    ncclResult_t r = R.GroupStart();
+    for (int i = 0; i < G && r == ncclSuccess; ++i) {
+      hipStream_t s = (hipStream_t)gpr_ctx_stream(h->ctx[i]);
+      r = R.Broadcast(h->buf[i].pk, h->buf[i].pk, npk, ncclDouble, 0, h->comm[i], s);
+      if (r == ncclSuccess)
+        r = R.Broadcast(h->buf[i].wt, h->buf[i].wt, ns, ncclDouble, 0, h->comm[i], s);
+    }
+    const ncclResult_t r2 = R.GroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return mg_err(h, GPR_E_HIP, "RCCL broadcast: %s",
+                    R.GetErrorString(r != ncclSuccess ? r : r2));
+  }
+  // 3. receivers unpack; every device predicts its rows and copies them into the host arrays
+  rc = on_devices(h, [&](int i) -> int {
+    gpr_ctx_t c = h->ctx[i];
+    auto& b = h->buf[i];
+    if (bcast && i > 0) {
+      GPR_TRY(launch_pack(c, b.U, ns, ns, b.pk, false));
+      GPR_TRY(gpr_forget_factor(c));  // the inverses of this buffer's old contents are stale
+    }
+    int pieces[6];
+    const int np = gpr_shard_pieces(ne, G, i, var_lo, var_hi, pieces);
+    if (np < 0) return set_err(c, GPR_E_ARG, "bad shard");
+    GPR_TRY(split_predict_pieces(c, kinds, nk, hp, d, b.x, ns, b.U, ns, b.wt, b.xe, ne, b.xq, nq,
+                                 pieces, np, var_lo, var_hi, eps, b.mu, b.var));
+    hipStream_t s = (hipStream_t)gpr_ctx_stream(c);
+    for (int k = 0; k < np; ++k) {
+      const int lo = pieces[2 * k], hi = pieces[2 * k + 1];
+      HIP_TRY(c, hipMemcpy2DAsync(mu + lo, sizeof(double) * ne, b.mu + lo, sizeof(double) * ne,
+                                  sizeof(double) * (hi - lo), nq, hipMemcpyDeviceToHost, s));
+      HIP_TRY(c, hipMemcpyAsync(var + (size_t)lo * nq, b.var + (size_t)lo * nq,
+                                sizeof(double) * (size_t)(hi - lo) * nq, hipMemcpyDeviceToHost, s));
+    }
+    return gpr_sync(c);
+  });
+  for (int i = 0; i < G; ++i)
+    if (rc[i] != 0)
+      return mg_err(h, rc[i] < 0 ? rc[i] : GPR_E_HIP, "device %d: %s", h->dev[i],
+                    gpr_last_error(h->ctx[i]));
+  return 0;
+}
+
+}  // extern "C"

@@ -752,36 +752,52 @@ int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
   return 0;
 }
 
-// Split factors of grid rows [e_lo, e_lo + E) into ctx->dbig2: per SE part p, A_p (E x nq),
-// BT_p (ns x E), C_p (ns x nq) (src/split_kernel.jl:151-159)
-static int split_build_factors(gpr_ctx* ctx, const KParams& kp, int d, const double* dX, int ns,
-                               const double* dXe, int e_lo, int E, const double* dXq, int nq,
-                               double** A, double** BT, double** C) {
+}  // extern "C"
+
+// Split prediction of several contiguous pieces of grid rows in one call (a rank's shard,
+// multi-GPU; gpr_split_predict is the one-piece case).  Factors (src/split_kernel.jl:151-159)
+// per SE part p: C_p (ns x nq, sigma^2, SplitDistanceC) built ONCE per call; A_p (E x nq,
+// sigma = 1, SplitDistanceA) and B_p^T (ns x E, sigma = 1, Euclidean) per piece of E rows.
+// Layout in ctx->dbig2: [C_0..C_{nse-1} | A_0.. | BT_0..] with the A/BT slots sized to the
+// largest piece.
+struct SplitFactors {
+  double *A, *BT, *C;
+  double *xs, *xes, *xqs;  // scaled inputs per part: (nse, ns, d), (nse, ne, d), (nse, nq, d)
+};
+
+static int split_prepare(gpr_ctx* ctx, const KParams& kp, int d, const double* dX, int ns,
+                         const double* dXe, int ne, const double* dXq, int nq, int Emax,
+                         SplitFactors* f) {
   const int nse = kp.nse;
-  const size_t szA = (size_t)E * nq, szB = (size_t)ns * E, szC = (size_t)ns * nq;
-  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap, (size_t)nse * (szA + szB + szC)));
-  *A = ctx->dbig2;
-  *BT = *A + nse * szA;
-  *C = *BT + nse * szB;
-  const size_t nxs = (size_t)nse * d * (ns + E + nq);
-  GPR_TRY(ensure_buf(ctx, &ctx->dxs, &ctx->xs_cap, nxs));
-  double* xs = ctx->dxs;
-  double* xes = xs + (size_t)nse * d * ns;
-  double* xqs = xes + (size_t)nse * d * E;
+  const size_t szC = (size_t)ns * nq;
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig2, &ctx->big2_cap,
+                     (size_t)nse * (szC + (size_t)Emax * nq + (size_t)ns * Emax)));
+  f->C = ctx->dbig2;
+  f->A = f->C + nse * szC;
+  f->BT = f->A + (size_t)nse * Emax * nq;
+  GPR_TRY(ensure_buf(ctx, &ctx->dxs, &ctx->xs_cap, (size_t)nse * d * (ns + ne + nq)));
+  f->xs = ctx->dxs;
+  f->xes = f->xs + (size_t)nse * d * ns;
+  f->xqs = f->xes + (size_t)nse * d * ne;
   TimerScope ts(ctx, TC_OTHER, 0.0);
-  GPR_TRY(launch_scale_inputs(ctx, kp, dX, ns, xs));
-  GPR_TRY(launch_scale_inputs(ctx, kp, dXe + (size_t)e_lo * d, E, xes));
-  GPR_TRY(launch_scale_inputs(ctx, kp, dXq, nq, xqs));
-  for (int p = 0; p < nse; ++p) {
-    const double s2 = kp.sigma[p] * kp.sigma[p];
-    // A: sigma = 1, SplitDistanceA(xe, xq); B: sigma = 1, Euclidean(xe, x) stored as B^T;
-    // C: sigma, SplitDistanceC(x, xq)
-    GPR_TRY(launch_pair(ctx, 1, d, xes + (size_t)p * d * E, E, xqs + (size_t)p * d * nq, nq, 1.0,
-                        *A + p * szA, 1, E));
-    GPR_TRY(launch_pair(ctx, 0, d, xes + (size_t)p * d * E, E, xs + (size_t)p * d * ns, ns, 1.0,
-                        *BT + p * szB, ns, 1));
-    GPR_TRY(launch_pair(ctx, 2, d, xs + (size_t)p * d * ns, ns, xqs + (size_t)p * d * nq, nq, s2,
-                        *C + p * szC, 1, ns));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dX, ns, f->xs));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dXe, ne, f->xes));
+  GPR_TRY(launch_scale_inputs(ctx, kp, dXq, nq, f->xqs));
+  for (int p = 0; p < nse; ++p)  // C: sigma, SplitDistanceC(x, xq)
+    GPR_TRY(launch_pair(ctx, 2, d, f->xs + (size_t)p * d * ns, ns, f->xqs + (size_t)p * d * nq, nq,
+                        kp.sigma[p] * kp.sigma[p], f->C + p * szC, 1, ns));
+  return 0;
+}
+
+// A and B^T of grid rows [e_lo, e_lo + E)
+static int split_piece_factors(gpr_ctx* ctx, const KParams& kp, int d, int ns, int ne, int nq,
+                               int e_lo, int E, const SplitFactors& f) {
+  TimerScope ts(ctx, TC_OTHER, 0.0);
+  const size_t szA = (size_t)E * nq, szB = (size_t)ns * E;
+  for (int p = 0; p < kp.nse; ++p) {
+    const double* xe = f.xes + ((size_t)p * ne + e_lo) * d;
+    GPR_TRY(launch_pair(ctx, 1, d, xe, E, f.xqs + (size_t)p * d * nq, nq, 1.0, f.A + p * szA, 1, E));
+    GPR_TRY(launch_pair(ctx, 0, d, xe, E, f.xs + (size_t)p * d * ns, ns, 1.0, f.BT + p * szB, ns, 1));
   }
   return 0;
 }
@@ -816,39 +832,73 @@ static int split_kxq(gpr_ctx* ctx, int nse, const double* A, const double* BT, c
   return 0;
 }
 
+int split_predict_pieces(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d,
+                         const double* dX, int ns, const double* dU, int ldu, const double* dwt,
+                         const double* dXe, int ne, const double* dXq, int nq, const int* pieces,
+                         int npieces, int var_lo, int var_hi, double eps, double* dmu,
+                         double* dvar) {
+  KParams kp;
+  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
+  if (ns <= 0 || ne <= 0 || nq <= 0 || ldu < ns || !dX || !dU || !dwt || !dXe || !dXq || !dmu ||
+      !dvar || npieces < 0 || (npieces && !pieces))
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  int Emax = 0;
+  for (int k = 0; k < npieces; ++k) {
+    const int lo = pieces[2 * k], hi = pieces[2 * k + 1];
+    if (lo < 0 || hi > ne || lo > hi) return set_err(ctx, GPR_E_ARG, "bad e range [%d,%d)", lo, hi);
+    if (k && lo < pieces[2 * k - 1])
+      return set_err(ctx, GPR_E_ARG, "pieces must be sorted and disjoint");
+    Emax = std::max(Emax, hi - lo);
+  }
+  if (Emax == 0) return 0;
+  const int nse = kp.nse;
+  SplitFactors f;
+  GPR_TRY(split_prepare(ctx, kp, d, dX, ns, dXe, ne, dXq, nq, Emax, &f));
+  const double prior = diag_prior(kinds, nk, hp, d);
+  const size_t per_row = (size_t)ns * nq;
+  for (int k = 0; k < npieces; ++k) {
+    const int e_lo = pieces[2 * k], e_hi = pieces[2 * k + 1], E = e_hi - e_lo;
+    if (E == 0) continue;
+    GPR_TRY(split_piece_factors(ctx, kp, d, ns, ne, nq, e_lo, E, f));
+    GPR_TRY(split_mean(ctx, nse, f.A, f.BT, f.C, ns, E, nq, dwt, dmu, e_lo, ne));
+    // ---- variance: prior everywhere in range, then rows e in [var_lo, var_hi) updated
+    GPR_TRY(launch_fill(ctx, dvar + (size_t)e_lo * nq, (size_t)E * nq, prior));
+    const int v0 = std::max(var_lo, e_lo), v1 = std::min(var_hi, e_hi);
+    if (v1 > v0) {
+      // <= 8 GiB of right-hand sides per batch (C5: 32 rows of ns = 32768, nq = 1024 in one
+      // U^{-T} solve of 32768 columns instead of four of 8192)
+      int Eb = (int)std::max<size_t>(1, ((size_t)1 << 30) / per_row);
+      Eb = std::min(Eb, v1 - v0);
+      GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per_row * Eb));
+      for (int e = v0; e < v1; e += Eb) {
+        const int nr = std::min(Eb, v1 - e);
+        GPR_TRY(split_kxq(ctx, nse, f.A, f.BT, f.C, ns, nq, E, e - e_lo, nr, ctx->dbig));
+        GPR_TRY(trsm_ut_core(ctx, dU, ns, ldu, ctx->dbig, nr * nq, ns, dvar + (size_t)e * nq, 0));
+      }
+    }
+  }
+  return 0;
+}
+
+extern "C" {
+
 int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                       const double* dX, int ns, const double* dU, int ldu, const double* dwt,
                       const double* dXe, int ne, const double* dXq, int nq, int e_lo, int e_hi,
                       int var_lo, int var_hi, double eps, double* dmu, double* dvar) {
-  KParams kp;
-  GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
-  if (ns <= 0 || ne <= 0 || nq <= 0 || ldu < ns || !dX || !dU || !dwt || !dXe || !dXq || !dmu || !dvar)
-    return set_err(ctx, GPR_E_ARG, "bad args");
   if (e_lo < 0 || e_hi > ne || e_lo > e_hi) return set_err(ctx, GPR_E_ARG, "bad e range [%d,%d)", e_lo, e_hi);
-  const int E = e_hi - e_lo;
-  if (E == 0) return 0;
-  const int nse = kp.nse;
-  double *A, *BT, *C;
-  GPR_TRY(split_build_factors(ctx, kp, d, dX, ns, dXe, e_lo, E, dXq, nq, &A, &BT, &C));
-  GPR_TRY(split_mean(ctx, nse, A, BT, C, ns, E, nq, dwt, dmu, e_lo, ne));
-  // ---- variance: prior everywhere in range, then rows e in [var_lo, var_hi) updated
-  const double prior = diag_prior(kinds, nk, hp, d);
-  GPR_TRY(launch_fill(ctx, dvar + (size_t)e_lo * nq, (size_t)E * nq, prior));
-  const int v0 = std::max(var_lo, e_lo), v1 = std::min(var_hi, e_hi);
-  if (v1 > v0) {
-    const size_t per_row = (size_t)ns * nq;
-    // <= 8 GiB of right-hand sides per batch (C5: 32 rows of ns = 32768, nq = 1024 in one
-    // U^{-T} solve of 32768 columns instead of four of 8192)
-    int Eb = (int)std::max<size_t>(1, ((size_t)1 << 30) / per_row);
-    Eb = std::min(Eb, v1 - v0);
-    GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per_row * Eb));
-    for (int e = v0; e < v1; e += Eb) {
-      const int nr = std::min(Eb, v1 - e);
-      GPR_TRY(split_kxq(ctx, nse, A, BT, C, ns, nq, E, e - e_lo, nr, ctx->dbig));
-      GPR_TRY(trsm_ut_core(ctx, dU, ns, ldu, ctx->dbig, nr * nq, ns, dvar + (size_t)e * nq, 0));
-    }
-  }
-  return 0;
+  const int piece[2] = {e_lo, e_hi};
+  return split_predict_pieces(ctx, kinds, nk, hp, d, dX, ns, dU, ldu, dwt, dXe, ne, dXq, nq, piece,
+                              1, var_lo, var_hi, eps, dmu, dvar);
+}
+
+int gpr_split_predict_rows(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                           const double* dX, int ns, const double* dU, int ldu, const double* dwt,
+                           const double* dXe, int ne, const double* dXq, int nq, const int* pieces,
+                           int npieces, int var_lo, int var_hi, double eps, double* dmu,
+                           double* dvar) {
+  return split_predict_pieces(ctx, kinds, nk, hp, d, dX, ns, dU, ldu, dwt, dXe, ne, dXq, nq, pieces,
+                              npieces, var_lo, var_hi, eps, dmu, dvar);
 }
 
 }  // extern "C"

@@ -23,6 +23,8 @@ GPR_WN = 2
 GPR_CROSS = 0        # gpr_kernel `same`: kernel!(K, cov, hp, x, xp), x !== xp
 GPR_SELF = 1         # kernel!(K, cov, hp, x): eps per SE part + noise
 GPR_SAME_OBJECT = 2  # kernel!(K, cov, hp, x, x), x === xp: eps per SE part, no noise
+GPR_MGPU_BROADCAST = 0  # gpr_split_predict_mgpu fit modes
+GPR_MGPU_REPLICATE = 1
 GPR_PREDICT_MEAN = 0
 GPR_PREDICT_DIAG = 1
 GPR_PREDICT_FULL = 2
@@ -80,6 +82,17 @@ _SIGS = {
     "gpr_integrate_noise": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _i, _dp, _dp, _dp, _d, _dp,
                                  _dp]),
     "gpr_cv_batch": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _ip, _i, _ip, _i, _i, _i, _d, _dp]),
+    "gpr_split_predict_rows": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _ip,
+                                    _i, _i, _i, _d, _p, _p]),
+    "gpr_shard_pieces": (_i, [_i, _i, _i, _i, _i, _ip]),
+    "gpr_packed_upper_len": (c_size_t, [_i]),
+    "gpr_pack_upper": (_i, [_p, _p, _i, _i, _p]),
+    "gpr_unpack_upper": (_i, [_p, _p, _i, _p, _i]),
+    "gpr_mgpu_create": (_i, [_i, _ip, POINTER(c_void_p)]),
+    "gpr_mgpu_destroy": (_i, [_p]),
+    "gpr_mgpu_last_error": (ctypes.c_char_p, [_p]),
+    "gpr_split_predict_mgpu": (_i, [_p, _ip, _i, _dp, _i, _dp, _i, _dp, _dp, _i, _dp, _i, _i, _i, _d,
+                                    _i, _dp, _dp, _ip]),
     "gpr_split_factors": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _i, _i, _p, _p, _p]),
 }
 

@@ -28,6 +28,7 @@ gloo (tests/test_distributed.py) and runs on libgpr_hip.so with RCCL on the GPUs
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Tuple
 
 import numpy as np
@@ -38,7 +39,7 @@ from . import core
 from ._lib import GprError, PosDefException, lib
 
 __all__ = ["shard_rows", "shard_pieces", "pack_upper", "unpack_upper", "HipSplitBackend",
-           "split_predict_distributed"]
+           "split_predict_distributed", "MultiGPU", "split_predict_mgpu"]
 
 
 def shard_rows(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -96,6 +97,7 @@ class HipSplitBackend:
                     (which waits only on the current stream) sends the finished U / wt.
     receive():      order the context stream after the current stream, so the split
                     kernels read U / wt only once the collective's copies have landed.
+    received():     (receiving ranks) drop the context's cached factor inverses.
     predict_rows(): gpr_split_predict for grid rows [e_lo, e_hi) into full-layout device
                     buffers (mu: nq x ne tensor = ne x nq column-major; var: ne nq).
 
@@ -124,11 +126,17 @@ class HipSplitBackend:
 
     def receive(self):
         self.ctx.stream.wait_stream(torch.cuda.current_stream(self.device))
-        # the broadcast wrote U behind the context's back: a cached factor keyed on the same
-        # device pointer (a re-used allocation) must not serve this one
+
+    def received(self):
+        """On the receiving ranks: the broadcast wrote U behind the context's back, so a
+        cached factor keyed on the same device pointer (a re-used allocation) must not serve
+        this one (the block inverses are rebuilt from the received U)."""
         self.ctx.check(lib.gpr_forget_factor(self.ctx.h), "gpr_forget_factor")
 
-    def predict_rows(self, cm: core.Cmap, U, wt, e_lo: int, e_hi: int, v_lo: int, v_hi: int):
+    def predict_pieces(self, cm: core.Cmap, U, wt, pieces, v_lo: int, v_hi: int):
+        """All of this rank's row pieces in ONE gpr_split_predict_rows call (the ns x nq C
+        factor built once, one pair of output buffers).  Returns full-layout device buffers
+        of which only the rows in `pieces` are written."""
         md, ctx = self.md, self.ctx
         _, ne, nq = cm.shape
         mu = ctx.zeros(nq, ne)
@@ -136,12 +144,18 @@ class HipSplitBackend:
         kinds, nk = core._kinds_arr(md.covar)
         _, hpp = core._hp_arr(md.params)
         dxe, dxq = ctx.colmajor(cm.xe), ctx.colmajor(cm.xq)
-        ctx.check(lib.gpr_split_predict(ctx.h, kinds, nk, hpp, md.d, core._ptr(md.dx()), md.n,
-                                        core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
-                                        core._ptr(dxq), nq, e_lo, e_hi, v_lo, v_hi, self.eps,
-                                        core._ptr(mu), core._ptr(var)), "gpr_split_predict")
+        flat = [v for p in pieces for v in p]
+        arr = (ctypes.c_int * max(len(flat), 1))(*flat)
+        ctx.check(lib.gpr_split_predict_rows(ctx.h, kinds, nk, hpp, md.d, core._ptr(md.dx()), md.n,
+                                             core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
+                                             core._ptr(dxq), nq, arr, len(pieces), v_lo, v_hi,
+                                             self.eps, core._ptr(mu), core._ptr(var)),
+                  "gpr_split_predict_rows")
         ctx.sync()
         return mu, var
+
+    def predict_rows(self, cm: core.Cmap, U, wt, e_lo: int, e_hi: int, v_lo: int, v_hi: int):
+        return self.predict_pieces(cm, U, wt, [(e_lo, e_hi)], v_lo, v_hi)
 
 
 _PACK_NB = 128
@@ -244,6 +258,8 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
             del P
         dist.broadcast(wt, _src(group), group=group)
         _hook(backend, "receive")
+        if rank != 0:
+            _hook(backend, "received")
 
     # 2. this rank's grid rows (an even share of the variance rows and of the others) and
     #    the var_range rows inside them
@@ -258,8 +274,13 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
     off = 0
     err = None
     try:
-        for lo, hi in pieces[rank]:
-            mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+        mine = pieces[rank]
+        if mine and hasattr(backend, "predict_pieces"):  # one call for every piece
+            full = backend.predict_pieces(cm, U, wt, mine, v_lo, v_hi)
+            per_piece = [full] * len(mine)
+        else:
+            per_piece = [backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi) for lo, hi in mine]
+        for (lo, hi), (mu_full, var_full) in zip(mine, per_piece):
             if mu_sh is None:
                 mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
                 var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
@@ -292,4 +313,65 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
             mu[:, a:b] = mr[:, off:off + b - a]
             var[a * nq:b * nq] = vr[off * nq:(off + b - a) * nq]
             off += b - a
+    return mu.T.copy(), var
+
+
+# =========================================================================================
+# One process, several GPUs: the C ABI's own sharded path (gpr_split_predict_mgpu, mgpu.hip)
+# =========================================================================================
+class MultiGPU:
+    """gpr_mgpu_create(ngpu, devices): one context per device and an RCCL communicator over
+    them (ncclCommInitAll), for gpr_split_predict_mgpu.  Reuse across calls; close() frees."""
+
+    def __init__(self, devices):
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        rc = lib.gpr_mgpu_create(len(self.devices), arr, ctypes.byref(h))
+        if rc != 0:
+            raise GprError(f"gpr_mgpu_create({self.devices}) failed ({rc})")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.gpr_mgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def split_predict_mgpu(md: core.GPRModel, cm: core.Cmap, mg: MultiGPU,
+                       var_range: Optional[Tuple[int, int]] = (1, 3), fit: str = "broadcast",
+                       eps: float = core.EPS_DEFAULT):
+    """predict(md, Cmap(+, xe, xq); diagonal_var=true) over the GPUs of `mg` in this one
+    process (host arrays in and out).  Returns (mu ne x nq, var ne nq) like
+    split_predict_distributed."""
+    if md.y.ndim != 1:
+        raise ValueError("split prediction needs a 1-D y (Diagonal(wt), src/split_predict.jl:13)")
+    mode = {"broadcast": 0, "replicate": 1}[fit]
+    _, ne, nq = cm.shape
+    v_lo, v_hi = var_rows(var_range, ne)
+    kinds, nk = core._kinds_arr(md.covar)
+    _, hpp = core._hp_arr(md.params)
+    D = ctypes.POINTER(ctypes.c_double)
+    c = lambda a: np.ascontiguousarray(a, dtype=np.float64)  # noqa: E731
+    X = c(md.x.T)          # d x ns column-major == ns x d row-major
+    y = c(md.y)
+    Xe, Xq = c(cm.xe.T), c(cm.xq.T)
+    mu = np.empty((nq, ne))  # ne x nq column-major
+    var = np.empty(ne * nq)
+    info = ctypes.c_int(0)
+    rc = lib.gpr_split_predict_mgpu(mg.h, kinds, nk, hpp, md.d, X.ctypes.data_as(D), md.n,
+                                    y.ctypes.data_as(D), Xe.ctypes.data_as(D), ne,
+                                    Xq.ctypes.data_as(D), nq, v_lo, v_hi, eps, mode,
+                                    mu.ctypes.data_as(D), var.ctypes.data_as(D), ctypes.byref(info))
+    if info.value > 0:
+        raise PosDefException(info.value)
+    if rc != 0:
+        raise GprError(f"gpr_split_predict_mgpu failed ({rc}): "
+                       f"{lib.gpr_mgpu_last_error(mg.h).decode()}")
     return mu.T.copy(), var

@@ -264,6 +264,17 @@ int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
                       int nq, int e_lo, int e_hi, int var_lo, int var_hi, double eps,
                       double* dmu, double* dvar);
 
+/* gpr_split_predict over several pieces of grid rows at once: pieces = host array of
+ * npieces sorted, disjoint half-open ranges {lo_0, hi_0, lo_1, hi_1, ...} (a rank's shard:
+ * an even share of the variance rows plus an even share of the rest, gpr_shard_pieces).  The
+ * ns x nq C factor is built once per call instead of once per piece; dmu / dvar index the
+ * full grid layout as in gpr_split_predict, only the rows in the pieces are written. */
+int gpr_split_predict_rows(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                           const double* dX, int ns, const double* dU, int ldu, const double* dwt,
+                           const double* dXe, int ne, const double* dXq, int nq, const int* pieces,
+                           int npieces, int var_lo, int var_hi, double eps, double* dmu,
+                           double* dvar);
+
 /* Split factors for inspection/tests (src/split_kernel.jl:151-159), SE part `part`
  * (0-based among SE parts): dA ne x nq, dB ne x ns, dC ns x nq (column-major,
  * leading dims = row counts). */
@@ -271,6 +282,46 @@ int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
                       const double* dX, int ns, const double* dXe, int ne,
                       const double* dXq, int nq, int part, double* dA, double* dB,
                       double* dC);
+
+/* ---- 8(e): split prediction sharded over the GPUs of one node, one host process ------- */
+/* Row pieces of grid row count n for `rank` of `world`: an even share of the variance rows
+ * [v_lo, v_hi) plus an even share of the others, as at most 3 sorted, disjoint, merged
+ * half-open ranges written to pieces[0..5] ({lo, hi} pairs).  Returns their number (or < 0).
+ * Host-only helper (no device work); the same partition as gpr_amd.distributed.shard_pieces. */
+int gpr_shard_pieces(int n, int world, int rank, int v_lo, int v_hi, int* pieces);
+
+/* The upper triangle of a column-major n x n factor packed by 128-column blocks (block
+ * [j0, j1) keeps rows [0, j1) of its columns): gpr_packed_upper_len(n) ~ n^2/2 + 64 n doubles,
+ * half the bytes of U for a broadcast.  Unpacking leaves the rest of dU untouched (no solve
+ * reads it).  A Julia MPI caller broadcasting pc.Kxx between processes uses these pairs, then
+ * gpr_forget_factor on the receivers. */
+size_t gpr_packed_upper_len(int n);
+int gpr_pack_upper(gpr_ctx_t ctx, const double* dU, int n, int ldu, double* dP);
+int gpr_unpack_upper(gpr_ctx_t ctx, const double* dP, int n, double* dU, int ldu);
+
+typedef struct gpr_mgpu* gpr_mgpu_t;
+#define GPR_MGPU_BROADCAST 0 /* device 0 fits; RCCL broadcast of packed U + wt (xGMI)   */
+#define GPR_MGPU_REPLICATE 1 /* every device fits for itself (no N^2 exchange)          */
+
+/* A set of ngpu devices (distinct ids) with one context each and an RCCL communicator
+ * (ncclCommInitAll; librccl.so.1 is dlopen'd: the process's own if loaded, else the
+ * system's).  Create once, reuse across calls. */
+int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out);
+int gpr_mgpu_destroy(gpr_mgpu_t h);
+const char* gpr_mgpu_last_error(gpr_mgpu_t h);
+
+/* predict(md, Cmap(+, xe, xq); diagonal_var=true) (src/predict.jl:14-25 ->
+ * src/split_predict.jl:5-53) sharded over the handle's GPUs.  HOST arrays in and out (the
+ * reference's CPU arrays): X d x ns, y ns, Xe d x ne, Xq d x nq; mu ne x nq column-major
+ * (index e + q ne), var ne*nq (index e nq + q; rows outside [var_lo, var_hi) keep the prior).
+ * fit_mode GPR_MGPU_BROADCAST / GPR_MGPU_REPLICATE.  Device i computes the rows
+ * gpr_shard_pieces(ne, ngpu, i, var_lo, var_hi) and copies them into mu / var itself.
+ * Returns > 0 (and *info) when K is not positive definite.  With ngpu = 1 the result equals
+ * gpr_fit + gpr_split_predict on that device bit for bit. */
+int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double* hp, int d,
+                           const double* X, int ns, const double* y, const double* Xe, int ne,
+                           const double* Xq, int nq, int var_lo, int var_hi, double eps,
+                           int fit_mode, double* mu, double* var, int* info);
 
 #ifdef __cplusplus
 }

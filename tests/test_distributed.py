@@ -310,3 +310,78 @@ def test_split_predict_distributed_shard_failure(tmp_path, fit):
     res = [open(tmp_path / f"r{r}.txt").read() for r in range(world)]
     assert res[1].startswith("RuntimeError"), res
     assert res[0].startswith("GprError") and res[2].startswith("GprError"), res
+
+
+def test_c_shard_pieces_matches_python():
+    """gpr_shard_pieces (mgpu.hip, host-only C) is the same partition as shard_pieces: the C
+    ABI's sharded path and the torch.distributed path give every device the same rows."""
+    import ctypes
+    from gpr_amd import _lib
+    out = (ctypes.c_int * 6)()
+    for n in range(0, 34):
+        for world in range(1, 9):
+            for v_lo in range(0, n + 1, 3):
+                for v_hi in (v_lo, min(n, v_lo + 1), min(n, v_lo + 5), n):
+                    for r in range(world):
+                        k = _lib.lib.gpr_shard_pieces(n, world, r, v_lo, v_hi, out)
+                        assert [(out[2 * i], out[2 * i + 1]) for i in range(k)] == \
+                            gd.shard_pieces(n, world, r, v_lo, v_hi)
+    assert _lib.lib.gpr_shard_pieces(5, 0, 0, 0, 0, out) < 0
+    for n in (0, 1, 127, 128, 129, 300, 32768):
+        assert _lib.lib.gpr_packed_upper_len(n) == gd._packed_len(n)
+
+
+@pytest.mark.gpu
+def test_pack_unpack_upper_device_roundtrip():
+    """gpr_pack_upper / gpr_unpack_upper (the broadcast's packed layout) against pack_upper,
+    and the round trip restores the upper triangle, leaving the rest untouched."""
+    import ctypes
+    G = pytest.importorskip("gpr_amd")
+    from gpr_amd import _lib
+    ctx = G.Context(0)
+    for n in (1, 127, 128, 300, 1000):
+        U = torch.from_numpy(np.random.default_rng(n).random((n, n))).to(ctx.device)
+        P = ctx.empty(_lib.lib.gpr_packed_upper_len(n))
+        assert _lib.lib.gpr_pack_upper(ctx.h, ctypes.c_void_p(U.data_ptr()), n, n,
+                                       ctypes.c_void_p(P.data_ptr())) == 0
+        ctx.sync()
+        assert torch.equal(P.cpu(), gd.pack_upper(U.cpu()))
+        V = torch.full((n, n), -7.0, dtype=torch.float64, device=ctx.device)
+        assert _lib.lib.gpr_unpack_upper(ctx.h, ctypes.c_void_p(P.data_ptr()), n,
+                                         ctypes.c_void_p(V.data_ptr()), n) == 0
+        ctx.sync()
+        Uc, Vc = U.cpu(), V.cpu()
+        for c in range(n):
+            assert torch.equal(Vc[c, :c + 1], Uc[c, :c + 1])
+            assert torch.all(Vc[c, (c // 128 + 1) * 128:] == -7.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fit", ["broadcast", "replicate"])
+def test_split_predict_mgpu_one_device(fit):
+    """gpr_split_predict_mgpu with ngpu = 1 equals gpr_fit + gpr_split_predict on that device
+    bit for bit (the one-GPU box cannot run more; the shard partition is tested against the
+    Python path above and the multi-rank logic with gloo), and matches the oracle."""
+    G = pytest.importorskip("gpr_amd")
+    kinds, hp, x, y, xe, xq = _problem(ne=13, nq=17, ns=700, d=4, seed=8)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    mg = gd.MultiGPU([0])
+    try:
+        for vr in ((1, 3), (2, 13), None):
+            mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=vr, fit=fit)
+            mu1, var1 = G.predict(md, cm, diagonal_var=True,
+                                  var_range=vr if vr is not None else (1, 0))
+            assert np.array_equal(mu, mu1) and np.array_equal(var, var1)
+        mu_o, var_o = O.split_predict(kinds, hp, x, y, xe, xq, var_range=(2, 13))
+        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(2, 13), fit=fit)
+        np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+        np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-8)
+        # a non positive definite K (eps = -1 cancels sigma^2 = 1 on the diagonal) -> info > 0
+        with pytest.raises(G.PosDefException):
+            gd.split_predict_mgpu(G.GPRModel(G.SquaredExp(), np.r_[1.0, hp[1:-1]], x, y), cm, mg,
+                                  fit=fit, eps=-1.0)
+    finally:
+        mg.close()
+    with pytest.raises(G.GprError):  # one rank per GPU
+        gd.MultiGPU([0, 0])

@@ -342,11 +342,13 @@ def test_pack_unpack_upper_device_roundtrip():
     for n in (1, 127, 128, 300, 1000):
         U = torch.from_numpy(np.random.default_rng(n).random((n, n))).to(ctx.device)
         P = ctx.empty(_lib.lib.gpr_packed_upper_len(n))
+        torch.cuda.synchronize()  # U was written on torch's stream, the calls run on ctx's
         assert _lib.lib.gpr_pack_upper(ctx.h, ctypes.c_void_p(U.data_ptr()), n, n,
                                        ctypes.c_void_p(P.data_ptr())) == 0
         ctx.sync()
         assert torch.equal(P.cpu(), gd.pack_upper(U.cpu()))
         V = torch.full((n, n), -7.0, dtype=torch.float64, device=ctx.device)
+        torch.cuda.synchronize()
         assert _lib.lib.gpr_unpack_upper(ctx.h, ctypes.c_void_p(P.data_ptr()), n,
                                          ctypes.c_void_p(V.data_ptr()), n) == 0
         ctx.sync()

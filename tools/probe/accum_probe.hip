@@ -58,7 +58,13 @@ __global__ __launch_bounds__(NW * 64, 1) void accum_kernel(const double* __restr
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < RB; ++j) acc[i][j] = d4v{0, 0, 0, 0};
+    for (int j = 0; j < RB; ++j) {
+      if (NW == 4)  // one wave per SIMD: accumulators defined in AGPRs (gemm.hip's idiom), so
+                    // the loop never copies them between register files
+        asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(0.0));
+      else
+        acc[i][j] = d4v{0, 0, 0, 0};
+    }
   const double* srcP[NDP];
   const double* srcQ[NDQ];
 #pragma unroll

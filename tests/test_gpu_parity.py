@@ -76,6 +76,19 @@ def test_kernel_matrix(name, n, d):
     assert Kx.shape == (n, 2 * n)
 
 
+@pytest.mark.parametrize("n,d", [(1, 3), (130, 2), (300, 8), (1000, 5), (2049, 8), (257, 17)])
+def test_kernel_matrix_ragged_tiles(n, d):
+    """The symmetric Gram K-assembly with ragged last tiles: same values as the oracle, K bitwise
+    symmetric, composed parts + noise."""
+    rng = np.random.default_rng(n + d)
+    x = rng.random((d, n))
+    for kinds in ([SE], [SE, SE, WN]):
+        hp = rand_hp(kinds, d, rng)
+        K = G.kernel(cov_of(kinds), hp, x)
+        np.testing.assert_allclose(K, O.kernel(kinds, hp, x), rtol=1e-13, atol=1e-15)
+        assert np.array_equal(K, K.T)
+
+
 def test_kernel_structure_isposdef():
     """test/test_covariance.jl:27-32: issymmetric, isposdef, shapes."""
     rng = np.random.default_rng(5)

@@ -299,7 +299,11 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   if (fit_mode != GPR_MGPU_BROADCAST && fit_mode != GPR_MGPU_REPLICATE)
     return mg_err(h, GPR_E_ARG, "fit_mode %d is neither GPR_MGPU_BROADCAST nor _REPLICATE", fit_mode);
   const int G = h->ngpu;
-  const bool bcast = fit_mode == GPR_MGPU_BROADCAST && G > 1;
+  // GPR_MGPU_SELF_BCAST=1 (tests on a one-GPU box): the broadcast path even for one device,
+  // which then also acts as a receiver (pack, 1-rank RCCL broadcast, unpack, forget)
+  const char* sb = getenv("GPR_MGPU_SELF_BCAST");
+  const bool self_bcast = sb && atoi(sb) != 0;
+  const bool bcast = fit_mode == GPR_MGPU_BROADCAST && (G > 1 || self_bcast);
   const size_t npk = packed_len(ns);
   std::vector<int> finfo(G, 0);
   // 1. inputs up, fit (device 0, or every device), device 0 packs U for the broadcast
@@ -351,7 +355,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   rc = on_devices(h, [&](int i) -> int {
     gpr_ctx_t c = h->ctx[i];
     auto& b = h->buf[i];
-    if (bcast && i > 0) {
+    if (bcast && (i > 0 || self_bcast)) {
       GPR_TRY(launch_pack(c, b.U, ns, ns, b.pk, false));
       GPR_TRY(gpr_forget_factor(c));  // the inverses of this buffer's old contents are stale
     }

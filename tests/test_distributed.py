@@ -387,3 +387,24 @@ def test_split_predict_mgpu_one_device(fit):
         mg.close()
     with pytest.raises(G.GprError):  # one rank per GPU
         gd.MultiGPU([0, 0])
+
+
+@pytest.mark.gpu
+def test_split_predict_mgpu_broadcast_path_one_device(monkeypatch):
+    """The broadcast path of gpr_split_predict_mgpu on the one-GPU box (GPR_MGPU_SELF_BCAST):
+    device 0 packs U, runs the 1-rank RCCL broadcast of the packed factor and wt, unpacks into
+    U as a receiver does and drops its cached block inverses; the result equals the
+    single-device split predict up to the rebuilt inverses' rounding (rtol 1e-12)."""
+    G = pytest.importorskip("gpr_amd")
+    monkeypatch.setenv("GPR_MGPU_SELF_BCAST", "1")
+    kinds, hp, x, y, xe, xq = _problem(ne=9, nq=33, ns=1500, d=5, seed=12)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    mg = gd.MultiGPU([0])
+    try:
+        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 9), fit="broadcast")
+    finally:
+        mg.close()
+    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 9))
+    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)

@@ -180,6 +180,156 @@ __global__ __launch_bounds__(NW * 64, 1) void accum_kernel(const double* __restr
 #endif
 }
 
+// Barrier-free variant: every wave DMAs its OWN operand rows (its 64 P rows and 64 Q rows)
+// into a private LDS region, so a wave waits only for its own DMA (vmcnt) and never for the
+// other waves (no s_barrier in the loop); each P / Q row is fetched by two waves (L2 hits).
+// PK-deep stages (8: 4 chunks per row, swizzle (row >> 2) & 3; 16: 8 chunks, (row >> 1) & 7),
+// NSTG stages, next stage's fragments prefetched into a second register set.
+template <int PK, int NSTG>
+__global__ __launch_bounds__(256, 1) void accum_priv_kernel(const double* __restrict__ M, size_t ld,
+                                                           int ncolblk, int nst, int mode,
+                                                           double* out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int NCH = PK / 2;              // 16-B chunks per LDS row
+  constexpr int RPD = 64 / NCH;            // rows per wave-wide 1-KB DMA
+  constexpr int ND = 64 / RPD;             // DMA per operand per wave per stage
+  constexpr int WSTAGE = 2 * 64 * PK;      // doubles per wave per stage (P rows, then Q rows)
+  constexpr int DNP = PK / 8;              // fragment blocks (2 k-steps each) per stage
+  constexpr int DVM = 2 * ND;
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  const int b = blockIdx.x;
+  const int np_ = ncolblk - 2;
+  const int pp = mode ? (b / 32) % np_ : 0, qp = mode ? 1 + (b % np_) : 1;
+  const double* P = M + (size_t)pp * DT * ld + (size_t)wm * 64 * ld;
+  const double* Q = M + (size_t)qp * DT * ld + (size_t)wn * 64 * ld;
+  auto sw = [](int row) { return PK == 8 ? ((row >> 2) & 3) : ((row >> 1) & 7); };
+  d4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(0.0));
+  const double* srcP[ND];
+  const double* srcQ[ND];
+#pragma unroll
+  for (int r = 0; r < ND; ++r) {
+    const int row = RPD * r + lane / NCH;
+    const int c = (lane % NCH) ^ sw(row);
+    srcP[r] = P + 2 * c + (size_t)row * ld;
+    srcQ[r] = Q + 2 * c + (size_t)row * ld;
+  }
+  double* mine = lds + w * WSTAGE;
+  auto issue = [&](int s) {
+    double* base = mine + (s % NSTG) * 4 * WSTAGE;
+    const size_t ko = (size_t)min(s, nst - 1) * PK;
+#pragma unroll
+    for (int r = 0; r < ND; ++r) {
+      __builtin_amdgcn_global_load_lds(srcP[r] + ko, base + r * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(srcQ[r] + ko, base + 64 * PK + r * 128, 16, 0, 0);
+    }
+  };
+  auto read_frags = [&](d2 (&F)[DNP][8], int s) {
+    const double* ps = mine + (s % NSTG) * 4 * WSTAGE;
+    const double* qs = ps + 64 * PK;
+#pragma unroll
+    for (int p = 0; p < DNP; ++p) {
+      const int ch = (lane >> 4) + 4 * p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = i * 16 + (lane & 15);
+        F[p][i] = *reinterpret_cast<const d2*>(&qs[row * PK + 2 * (ch ^ sw(row))]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = j * 16 + (lane & 15);
+        F[p][4 + j] = *reinterpret_cast<const d2*>(&ps[row * PK + 2 * (ch ^ sw(row))]);
+      }
+    }
+  };
+  auto mfma_stage = [&](const d2 (&F)[DNP][8]) {
+#pragma unroll
+    for (int p = 0; p < DNP; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[p][i][h], F[p][4 + j][h], acc[i][j], 0, 0, 0);
+  };
+  auto step = [&](int s, d2 (&Fc)[DNP][8], d2 (&Fn)[DNP][8]) {
+    __builtin_amdgcn_sched_barrier(0);
+    // stage s - 1's buffer: its fragments were read (and waited for) a step ago
+    issue(s + NSTG - 1);
+    vmcnt<DVM * (NSTG - 2)>();  // own DMA of stage s + 1 landed (s + 2 .. s + NSTG - 1 in flight)
+    read_frags(Fn, s + 1);
+    mfma_stage(Fc);
+#pragma unroll
+    for (int t = 0; t < 8 * DNP; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 32 * DNP - 16 * DNP, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): Fn in registers before the next issue
+  };
+  d2 F0[DNP][8], F1[DNP][8];
+#pragma unroll
+  for (int t = 0; t < NSTG - 1; ++t) issue(t);
+  vmcnt<DVM * (NSTG - 2)>();
+  read_frags(F0, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  int s = 0;
+  for (; s + 1 < nst; s += 2) {
+    step(s, F0, F1);
+    step(s + 1, F1, F0);
+  }
+  if (s < nst) mfma_stage(F0);
+  vmcnt<0>();
+  double t = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  out[blockIdx.x * 512 + tid] = t;
+#endif
+}
+
+template <int PK, int NSTG>
+void run_priv(const double* M, size_t ld, int ncolblk, int K, int reps, int mode, double* out, int cus) {
+  constexpr size_t lds = sizeof(double) * NSTG * 4 * 2 * 64 * PK;
+  if (hipFuncSetAttribute((const void*)accum_priv_kernel<PK, NSTG>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    printf("priv PK=%d NSTG=%d: cannot set %zu B of LDS\n", PK, NSTG, lds);
+    return;
+  }
+  const int nst = K / PK;
+  hipLaunchKernelGGL((accum_priv_kernel<PK, NSTG>), dim3(cus), dim3(256), lds, 0, M, ld, ncolblk, 8, mode, out);
+  hipError_t le = hipGetLastError();
+  if (le == hipSuccess) le = hipDeviceSynchronize();
+  if (le != hipSuccess) {
+    printf("priv PK=%d NSTG=%d: launch failed: %s\n", PK, NSTG, hipGetErrorString(le));
+    return;
+  }
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0);
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((accum_priv_kernel<PK, NSTG>), dim3(cus), dim3(256), lds, 0, M, ld, ncolblk, nst, mode, out);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  const double flops = 2.0 * DT * DT * (double)nst * PK * cus * reps;
+  printf("%s private-buffer 128x128, 4 waves, %2d-deep x %d stages (%3zu KB), no barrier: "
+         "%.2f TFLOP/s = %.4f per CU (%.3f ms per launch)\n", mode ? "dag-like" : "hot     ",
+         PK, NSTG, lds / 1024, flops / ms / 1e9, flops / ms / 1e9 / cus, ms / reps);
+}
+
 template <int TMR, int NW, int NSTG, bool DBUF>
 void run(const double* M, size_t ld, int ncolblk, int K, int reps, int mode, double* out, int cus) {
   constexpr size_t lds = sizeof(double) * NSTG * (DT * TMR + DT) * DTK;
@@ -238,6 +388,9 @@ int main(int argc, char** argv) {
     case 1: run<2, 4, 3, false>(M, ld, ncolblk, K, reps, mode, out, cus); break;  // 256 x 128, 1 wave/SIMD
     case 2: run<2, 8, 3, false>(M, ld, ncolblk, K, reps, mode, out, cus); break;  // 256 x 128, 2 waves/SIMD
     case 3: run<1, 4, 4, false>(M, ld, ncolblk, K, reps, mode, out, cus); break;
+    case 4: run_priv<8, 4>(M, ld, ncolblk, K, reps, mode, out, cus); break;   // 128 KB
+    case 5: run_priv<8, 5>(M, ld, ncolblk, K, reps, mode, out, cus); break;   // 160 KB
+    case 6: run_priv<16, 2>(M, ld, ncolblk, K, reps, mode, out, cus); break;  // 128 KB
   }
   return 0;
 }

@@ -173,12 +173,17 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
       const int c = dl ? lane : 32 + 32 * wv + (lane - 32);  // band column (D / strip)
       const int q = lane - 32;                                // identity column
       double x[32];
+      // all 32 loads first, unconditionally (identity lanes read any valid address), then the
+      // selects: with the select next to each load the compiler put every load in its own
+      // exec-masked branch with its own lgkmcnt(0) wait -- 32 serialised LDS round trips
 #pragma unroll
       for (int r = 0; r < 32; ++r) {
-        const int cc = il ? r : c;  // any valid address for identity lanes
-        const double sv = S[pk(K0 + min(r, cc), K0 + cc)];
-        x[r] = il ? (r == q ? 1.0 : 0.0) : ((dl && r > lane) ? 0.0 : sv);
+        const int cc = il ? r : c;
+        x[r] = S[pk(K0 + min(r, cc), K0 + cc)];
       }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < 32; ++r) x[r] = il ? (r == q ? 1.0 : 0.0) : ((dl && r > lane) ? 0.0 : x[r]);
       int bad = 0;
 #pragma unroll
       for (int j = 0; j < 32; ++j) {

@@ -167,8 +167,8 @@ struct gpr_ctx {
 int split_predict_pieces(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d,
                          const double* dX, int ns, const double* dU, int ldu, const double* dwt,
                          const double* dXe, int ne, const double* dXq, int nq, const int* pieces,
-                         int npieces, int var_lo, int var_hi, double eps, double* dmu,
-                         double* dvar);
+                         int npieces, int var_lo, int var_hi, double eps, double* dmu, int ldmu,
+                         double* dvar, bool compact);
 int set_err(gpr_ctx* ctx, int code, const char* fmt, ...);
 
 #define HIP_TRY(ctx, expr)                                                          \

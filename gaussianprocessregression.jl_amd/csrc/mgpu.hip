@@ -12,7 +12,8 @@
 //   2. rows -- device i takes gpr_shard_pieces(ne, ngpu, i, var_lo, var_hi): an even share of
 //              the variance rows (an ns^2 triangular solve per test point) and of the mean-only
 //              rows, as at most three contiguous pieces, all in one split_predict_pieces call
-//              (the ns x nq C factor built once per device).
+//              (the ns x nq C factor built once per device), into output buffers sized to
+//              the device's rows (compact: pieces concatenated), not to the grid.
 //   3. out  -- every device copies its rows of mu (ne x nq column-major, index e + q ne) and of
 //              the variance diagonal (index e nq + q) straight into the caller's host arrays
 //              (each GPU over its own PCIe link; no gather through one device).
@@ -23,6 +24,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -306,6 +308,14 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   const bool bcast = fit_mode == GPR_MGPU_BROADCAST && (G > 1 || self_bcast);
   const size_t npk = packed_len(ns);
   std::vector<int> finfo(G, 0);
+  // each device's row pieces (its output buffers hold just these rows)
+  std::vector<std::array<int, 6>> pcs(G);
+  std::vector<int> npc(G), rows(G, 0);
+  for (int i = 0; i < G; ++i) {
+    npc[i] = gpr_shard_pieces(ne, G, i, var_lo, var_hi, pcs[i].data());
+    if (npc[i] < 0) return mg_err(h, GPR_E_ARG, "bad shard");
+    for (int k = 0; k < npc[i]; ++k) rows[i] += pcs[i][2 * k + 1] - pcs[i][2 * k];
+  }
   // 1. inputs up, fit (device 0, or every device), device 0 packs U for the broadcast
   auto rc = on_devices(h, [&](int i) -> int {
     gpr_ctx_t c = h->ctx[i];
@@ -313,7 +323,8 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     if (!grow(&b.x, &b.cx, (size_t)d * ns) || !grow(&b.y, &b.cy, ns) ||
         !grow(&b.xe, &b.cxe, (size_t)d * ne) || !grow(&b.xq, &b.cxq, (size_t)d * nq) ||
         !grow(&b.U, &b.cU, (size_t)ns * ns) || !grow(&b.wt, &b.cwt, ns) ||
-        !grow(&b.mu, &b.cmu, (size_t)ne * nq) || !grow(&b.var, &b.cvar, (size_t)ne * nq) ||
+        !grow(&b.mu, &b.cmu, (size_t)std::max(rows[i], 1) * nq) ||
+        !grow(&b.var, &b.cvar, (size_t)std::max(rows[i], 1) * nq) ||
         (bcast && !grow(&b.pk, &b.cpk, npk)))
       return set_err(c, GPR_E_NOMEM, "device %d: allocation failed", h->dev[i]);
     GPR_TRY(gpr_upload(c, b.x, X, sizeof(double) * d * ns));
@@ -359,17 +370,17 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
       GPR_TRY(launch_pack(c, b.U, ns, ns, b.pk, false));
       GPR_TRY(gpr_forget_factor(c));  // the inverses of this buffer's old contents are stale
     }
-    int pieces[6];
-    const int np = gpr_shard_pieces(ne, G, i, var_lo, var_hi, pieces);
-    if (np < 0) return set_err(c, GPR_E_ARG, "bad shard");
+    const int* pieces = pcs[i].data();
+    const int np = npc[i], R = std::max(rows[i], 1);
+    // the shard's rows only (compact: piece k's rows at off_k, mu leading dimension R)
     GPR_TRY(split_predict_pieces(c, kinds, nk, hp, d, b.x, ns, b.U, ns, b.wt, b.xe, ne, b.xq, nq,
-                                 pieces, np, var_lo, var_hi, eps, b.mu, b.var));
+                                 pieces, np, var_lo, var_hi, eps, b.mu, R, b.var, true));
     hipStream_t s = (hipStream_t)gpr_ctx_stream(c);
-    for (int k = 0; k < np; ++k) {
+    for (int k = 0, off = 0; k < np; off += pieces[2 * k + 1] - pieces[2 * k], ++k) {
       const int lo = pieces[2 * k], hi = pieces[2 * k + 1];
-      HIP_TRY(c, hipMemcpy2DAsync(mu + lo, sizeof(double) * ne, b.mu + lo, sizeof(double) * ne,
+      HIP_TRY(c, hipMemcpy2DAsync(mu + lo, sizeof(double) * ne, b.mu + off, sizeof(double) * R,
                                   sizeof(double) * (hi - lo), nq, hipMemcpyDeviceToHost, s));
-      HIP_TRY(c, hipMemcpyAsync(var + (size_t)lo * nq, b.var + (size_t)lo * nq,
+      HIP_TRY(c, hipMemcpyAsync(var + (size_t)lo * nq, b.var + (size_t)off * nq,
                                 sizeof(double) * (size_t)(hi - lo) * nq, hipMemcpyDeviceToHost, s));
     }
     return gpr_sync(c);

@@ -804,8 +804,9 @@ static int split_piece_factors(gpr_ctx* ctx, const KParams& kp, int d, int ns, i
 
 // mu[e, q] = sum_p A_p[e,q] * (B_p diag(wt) C_p)[e,q] for rows [e_lo, e_lo + E)
 // (src/split_predict.jl:10-19)
+// (dmu: output row of e_lo, leading dimension ldmu)
 static int split_mean(gpr_ctx* ctx, int nse, const double* A, const double* BT, const double* C,
-                      int ns, int E, int nq, const double* dwt, double* dmu, int e_lo, int ne) {
+                      int ns, int E, int nq, const double* dwt, double* dmu, int ldmu) {
   const size_t szA = (size_t)E * nq, szB = (size_t)ns * E, szC = (size_t)ns * nq;
   for (int p = 0; p < nse; ++p) {
     GemmArgs g{};
@@ -813,7 +814,7 @@ static int split_mean(gpr_ctx* ctx, int nse, const double* A, const double* BT, 
     g.Q = C + p * szC; g.ldq = ns;
     g.qscale = dwt;
     g.E = A + p * szA; g.lde = E;
-    g.C = dmu + e_lo; g.ldc = ne;
+    g.C = dmu; g.ldc = ldmu;
     g.M = E; g.N = nq; g.K = ns;
     g.alpha = 1.0; g.beta = (p == 0) ? 0.0 : 1.0;
     GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
@@ -832,37 +833,44 @@ static int split_kxq(gpr_ctx* ctx, int nse, const double* A, const double* BT, c
   return 0;
 }
 
+// Output rows: full grid layout (compact = false: row e at e, dmu leading dim ldmu = ne) or
+// the shard's rows only (compact: the pieces' rows concatenated in order, row e of piece k at
+// off_k + e - lo_k; dmu R x nq with leading dim ldmu >= R, dvar R nq).
 int split_predict_pieces(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d,
                          const double* dX, int ns, const double* dU, int ldu, const double* dwt,
                          const double* dXe, int ne, const double* dXq, int nq, const int* pieces,
-                         int npieces, int var_lo, int var_hi, double eps, double* dmu,
-                         double* dvar) {
+                         int npieces, int var_lo, int var_hi, double eps, double* dmu, int ldmu,
+                         double* dvar, bool compact) {
   KParams kp;
   GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
   if (ns <= 0 || ne <= 0 || nq <= 0 || ldu < ns || !dX || !dU || !dwt || !dXe || !dXq || !dmu ||
       !dvar || npieces < 0 || (npieces && !pieces))
     return set_err(ctx, GPR_E_ARG, "bad args");
-  int Emax = 0;
+  int Emax = 0, R = 0;
   for (int k = 0; k < npieces; ++k) {
     const int lo = pieces[2 * k], hi = pieces[2 * k + 1];
     if (lo < 0 || hi > ne || lo > hi) return set_err(ctx, GPR_E_ARG, "bad e range [%d,%d)", lo, hi);
     if (k && lo < pieces[2 * k - 1])
       return set_err(ctx, GPR_E_ARG, "pieces must be sorted and disjoint");
     Emax = std::max(Emax, hi - lo);
+    R += hi - lo;
   }
+  if (ldmu < (compact ? std::max(R, 1) : ne))
+    return set_err(ctx, GPR_E_ARG, "ldmu %d < %d", ldmu, compact ? R : ne);
   if (Emax == 0) return 0;
   const int nse = kp.nse;
   SplitFactors f;
   GPR_TRY(split_prepare(ctx, kp, d, dX, ns, dXe, ne, dXq, nq, Emax, &f));
   const double prior = diag_prior(kinds, nk, hp, d);
   const size_t per_row = (size_t)ns * nq;
-  for (int k = 0; k < npieces; ++k) {
+  for (int k = 0, off = 0; k < npieces; off += pieces[2 * k + 1] - pieces[2 * k], ++k) {
     const int e_lo = pieces[2 * k], e_hi = pieces[2 * k + 1], E = e_hi - e_lo;
     if (E == 0) continue;
+    const int o = compact ? off : e_lo;  // output row of grid row e_lo
     GPR_TRY(split_piece_factors(ctx, kp, d, ns, ne, nq, e_lo, E, f));
-    GPR_TRY(split_mean(ctx, nse, f.A, f.BT, f.C, ns, E, nq, dwt, dmu, e_lo, ne));
+    GPR_TRY(split_mean(ctx, nse, f.A, f.BT, f.C, ns, E, nq, dwt, dmu + o, ldmu));
     // ---- variance: prior everywhere in range, then rows e in [var_lo, var_hi) updated
-    GPR_TRY(launch_fill(ctx, dvar + (size_t)e_lo * nq, (size_t)E * nq, prior));
+    GPR_TRY(launch_fill(ctx, dvar + (size_t)o * nq, (size_t)E * nq, prior));
     const int v0 = std::max(var_lo, e_lo), v1 = std::min(var_hi, e_hi);
     if (v1 > v0) {
       // <= 8 GiB of right-hand sides per batch (C5: 32 rows of ns = 32768, nq = 1024 in one
@@ -873,7 +881,8 @@ int split_predict_pieces(gpr_ctx* ctx, const int* kinds, int nk, const double* h
       for (int e = v0; e < v1; e += Eb) {
         const int nr = std::min(Eb, v1 - e);
         GPR_TRY(split_kxq(ctx, nse, f.A, f.BT, f.C, ns, nq, E, e - e_lo, nr, ctx->dbig));
-        GPR_TRY(trsm_ut_core(ctx, dU, ns, ldu, ctx->dbig, nr * nq, ns, dvar + (size_t)e * nq, 0));
+        GPR_TRY(trsm_ut_core(ctx, dU, ns, ldu, ctx->dbig, nr * nq, ns,
+                             dvar + (size_t)(o + e - e_lo) * nq, 0));
       }
     }
   }
@@ -889,7 +898,7 @@ int gpr_split_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp,
   if (e_lo < 0 || e_hi > ne || e_lo > e_hi) return set_err(ctx, GPR_E_ARG, "bad e range [%d,%d)", e_lo, e_hi);
   const int piece[2] = {e_lo, e_hi};
   return split_predict_pieces(ctx, kinds, nk, hp, d, dX, ns, dU, ldu, dwt, dXe, ne, dXq, nq, piece,
-                              1, var_lo, var_hi, eps, dmu, dvar);
+                              1, var_lo, var_hi, eps, dmu, ne, dvar, false);
 }
 
 int gpr_split_predict_rows(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
@@ -898,7 +907,16 @@ int gpr_split_predict_rows(gpr_ctx_t ctx, const int* kinds, int nk, const double
                            int npieces, int var_lo, int var_hi, double eps, double* dmu,
                            double* dvar) {
   return split_predict_pieces(ctx, kinds, nk, hp, d, dX, ns, dU, ldu, dwt, dXe, ne, dXq, nq, pieces,
-                              npieces, var_lo, var_hi, eps, dmu, dvar);
+                              npieces, var_lo, var_hi, eps, dmu, ne, dvar, false);
+}
+
+int gpr_split_predict_shard(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                            const double* dX, int ns, const double* dU, int ldu,
+                            const double* dwt, const double* dXe, int ne, const double* dXq,
+                            int nq, const int* pieces, int npieces, int var_lo, int var_hi,
+                            double eps, double* dmu, int ldmu, double* dvar) {
+  return split_predict_pieces(ctx, kinds, nk, hp, d, dX, ns, dU, ldu, dwt, dXe, ne, dXq, nq, pieces,
+                              npieces, var_lo, var_hi, eps, dmu, ldmu, dvar, true);
 }
 
 }  // extern "C"

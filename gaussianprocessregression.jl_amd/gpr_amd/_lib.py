@@ -84,6 +84,8 @@ _SIGS = {
     "gpr_cv_batch": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _ip, _i, _ip, _i, _i, _i, _d, _dp]),
     "gpr_split_predict_rows": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _ip,
                                     _i, _i, _i, _d, _p, _p]),
+    "gpr_split_predict_shard": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _ip,
+                                     _i, _i, _i, _d, _p, _i, _p]),
     "gpr_shard_pieces": (_i, [_i, _i, _i, _i, _i, _ip]),
     "gpr_packed_upper_len": (c_size_t, [_i]),
     "gpr_pack_upper": (_i, [_p, _p, _i, _i, _p]),

@@ -17,8 +17,9 @@ wt = K^{-1} y exist, so:
      var_range keep the prior.  A variance row costs an N^2 triangular solve per test point
      (N = 32768, nq = 1024: ~1.1e12 flop) against ~1e8 for a mean row, so a plain split of
      the grid rows would leave every variance row of the default var_range on rank 0.
-  3. the shards are all-gathered (mu: rows x nq per rank, var: rows nq, padded to the
-     largest share) and reassembled in the reference layouts: mu ne x nq column-major
+  3. every rank writes its rows straight into shard-sized buffers (mu: rows x nq, var:
+     rows nq, padded to the largest share -- never a grid-sized buffer per rank); the shards
+     are all-gathered and reassembled in the reference layouts: mu ne x nq column-major
      (linear e + q ne), var.diag index e nq + q.
 
 The collective sequence (broadcast, then all_gather) is the only data exchange; the
@@ -98,8 +99,9 @@ class HipSplitBackend:
     receive():      order the context stream after the current stream, so the split
                     kernels read U / wt only once the collective's copies have landed.
     received():     (receiving ranks) drop the context's cached factor inverses.
-    predict_rows(): gpr_split_predict for grid rows [e_lo, e_hi) into full-layout device
-                    buffers (mu: nq x ne tensor = ne x nq column-major; var: ne nq).
+    predict_shard(): all of the rank's row pieces in one gpr_split_predict_shard call, into
+                    shard-sized device buffers (mu: nq x emax tensor = emax x nq column-major,
+                    var: emax nq; the pieces' rows concatenated in order).
 
     gpr_fit returns once the factorisation's info is known, with the wt solve still queued
     on the context stream; RCCL runs on its own stream that waits on torch's current stream
@@ -133,29 +135,26 @@ class HipSplitBackend:
         this one (the block inverses are rebuilt from the received U)."""
         self.ctx.check(lib.gpr_forget_factor(self.ctx.h), "gpr_forget_factor")
 
-    def predict_pieces(self, cm: core.Cmap, U, wt, pieces, v_lo: int, v_hi: int):
-        """All of this rank's row pieces in ONE gpr_split_predict_rows call (the ns x nq C
-        factor built once, one pair of output buffers).  Returns full-layout device buffers
-        of which only the rows in `pieces` are written."""
+    def predict_shard(self, cm: core.Cmap, U, wt, pieces, v_lo: int, v_hi: int, emax: int):
+        """All of this rank's row pieces in ONE gpr_split_predict_shard call (the ns x nq C
+        factor built once) into buffers of emax rows (emax >= the shard's rows: the
+        all_gather's common size)."""
         md, ctx = self.md, self.ctx
         _, ne, nq = cm.shape
-        mu = ctx.zeros(nq, ne)
-        var = ctx.zeros(ne * nq)
+        mu = ctx.zeros(nq, emax)  # emax x nq column-major (leading dimension emax)
+        var = ctx.zeros(emax * nq)
         kinds, nk = core._kinds_arr(md.covar)
         _, hpp = core._hp_arr(md.params)
         dxe, dxq = ctx.colmajor(cm.xe), ctx.colmajor(cm.xq)
         flat = [v for p in pieces for v in p]
         arr = (ctypes.c_int * max(len(flat), 1))(*flat)
-        ctx.check(lib.gpr_split_predict_rows(ctx.h, kinds, nk, hpp, md.d, core._ptr(md.dx()), md.n,
-                                             core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
-                                             core._ptr(dxq), nq, arr, len(pieces), v_lo, v_hi,
-                                             self.eps, core._ptr(mu), core._ptr(var)),
-                  "gpr_split_predict_rows")
+        ctx.check(lib.gpr_split_predict_shard(ctx.h, kinds, nk, hpp, md.d, core._ptr(md.dx()), md.n,
+                                              core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
+                                              core._ptr(dxq), nq, arr, len(pieces), v_lo, v_hi,
+                                              self.eps, core._ptr(mu), emax, core._ptr(var)),
+                  "gpr_split_predict_shard")
         ctx.sync()
         return mu, var
-
-    def predict_rows(self, cm: core.Cmap, U, wt, e_lo: int, e_hi: int, v_lo: int, v_hi: int):
-        return self.predict_pieces(cm, U, wt, [(e_lo, e_hi)], v_lo, v_hi)
 
 
 _PACK_NB = 128
@@ -267,26 +266,28 @@ def split_predict_distributed(md: core.GPRModel, cm: core.Cmap,
     pieces = [shard_pieces(ne, world, r, v_lo, v_hi) for r in range(world)]
     rows = [sum(b - a for a, b in p) for p in pieces]
 
-    # 3. pack the rank's rows (piece order), all-gather padded shards, reassemble the
-    #    reference layouts
+    # 3. the rank's rows (piece order) into shard-sized buffers of emax rows, all-gather,
+    #    reassemble the reference layouts
     emax = max(max(rows), 1)
     mu_sh = var_sh = None
-    off = 0
     err = None
     try:
         mine = pieces[rank]
-        if mine and hasattr(backend, "predict_pieces"):  # one call for every piece
-            full = backend.predict_pieces(cm, U, wt, mine, v_lo, v_hi)
-            per_piece = [full] * len(mine)
-        else:
-            per_piece = [backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi) for lo, hi in mine]
-        for (lo, hi), (mu_full, var_full) in zip(mine, per_piece):
-            if mu_sh is None:
-                mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
-                var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
-            mu_sh[:, off:off + hi - lo] = mu_full[:, lo:hi]
-            var_sh[off * nq:(off + hi - lo) * nq] = var_full[lo * nq:hi * nq]
-            off += hi - lo
+        if mine and hasattr(backend, "predict_shard"):  # one call, shard-sized outputs
+            mu_sh, var_sh = backend.predict_shard(cm, U, wt, mine, v_lo, v_hi, emax)
+            if tuple(mu_sh.shape) != (nq, emax) or tuple(var_sh.shape) != (emax * nq,):
+                raise GprError(f"predict_shard returned {tuple(mu_sh.shape)} / "
+                               f"{tuple(var_sh.shape)}, expected ({nq}, {emax}) / ({emax * nq},)")
+        elif mine:  # generic backend: full-layout rows per piece, copied into the shard
+            off = 0
+            for lo, hi in mine:
+                mu_full, var_full = backend.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+                if mu_sh is None:
+                    mu_sh = torch.zeros(nq, emax, dtype=mu_full.dtype, device=mu_full.device)
+                    var_sh = torch.zeros(emax * nq, dtype=var_full.dtype, device=var_full.device)
+                mu_sh[:, off:off + hi - lo] = mu_full[:, lo:hi]
+                var_sh[off * nq:(off + hi - lo) * nq] = var_full[lo * nq:hi * nq]
+                off += hi - lo
     except Exception as e:  # noqa: BLE001 -- re-raised after the status exchange
         err = e
     # as for the fit: every rank learns of a failed shard before the all_gather, so all ranks

@@ -275,6 +275,17 @@ int gpr_split_predict_rows(gpr_ctx_t ctx, const int* kinds, int nk, const double
                            int npieces, int var_lo, int var_hi, double eps, double* dmu,
                            double* dvar);
 
+/* gpr_split_predict_rows with outputs sized to the shard, not to the grid: the pieces' R rows
+ * concatenated in piece order (row e of piece k at r = off_k + e - lo_k, off_k = rows of the
+ * pieces before it).  dmu: R x nq column-major, leading dimension ldmu >= R (index r + q*ldmu);
+ * dvar: R*nq (index r*nq + q).  What a rank of a multi-GPU split prediction allocates
+ * (R ~ ne / ngpu rows instead of ne). */
+int gpr_split_predict_shard(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
+                            const double* dX, int ns, const double* dU, int ldu,
+                            const double* dwt, const double* dXe, int ne, const double* dXq,
+                            int nq, const int* pieces, int npieces, int var_lo, int var_hi,
+                            double eps, double* dmu, int ldmu, double* dvar);
+
 /* Split factors for inspection/tests (src/split_kernel.jl:151-159), SE part `part`
  * (0-based among SE parts): dA ne x nq, dB ne x ns, dC ns x nq (column-major,
  * leading dims = row counts). */

@@ -85,20 +85,47 @@ class OracleBackend:
         return mu, var
 
 
-def _worker(rank, world, port, out, ne, nq, var_range, fit):
+class ShardOracleBackend(OracleBackend):
+    """The HIP backend's interface: predict_shard fills buffers sized to the rank's shard
+    (emax rows, the pieces' rows concatenated), never a grid-sized one.  Records the calls."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.calls = []
+
+    def predict_shard(self, cm, U, wt, pieces, v_lo, v_hi, emax):
+        _, ne, nq = cm.shape
+        self.calls.append((list(pieces), emax))
+        mu = torch.zeros(nq, emax, dtype=torch.float64)
+        var = torch.zeros(emax * nq, dtype=torch.float64)
+        off = 0
+        for lo, hi in pieces:
+            m_full, v_full = self.predict_rows(cm, U, wt, lo, hi, v_lo, v_hi)
+            mu[:, off:off + hi - lo] = m_full[:, lo:hi]
+            var[off * nq:(off + hi - lo) * nq] = v_full[lo * nq:hi * nq]
+            off += hi - lo
+        return mu, var
+
+
+def _worker(rank, world, port, out, ne, nq, var_range, fit, kind="rows"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         kinds, hp, x, y, xe, xq = _problem(ne=ne, nq=nq)
-        be = OracleBackend(kinds, hp, x, y, allow_fit=(fit == "replicate" or rank == 0))
+        cls = ShardOracleBackend if kind == "shard" else OracleBackend
+        be = cls(kinds, hp, x, y, allow_fit=(fit == "replicate" or rank == 0))
         mu, var = gd.split_predict_distributed(None, _Cmap(xe, xq), var_range=var_range,
                                                backend=be, fit=fit)
         np.save(os.path.join(out, f"mu{rank}.npy"), mu)
         np.save(os.path.join(out, f"var{rank}.npy"), var)
+        if kind == "shard":
+            with open(os.path.join(out, f"calls{rank}.txt"), "w") as f:
+                f.write(repr(be.calls))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("kind", ["rows", "shard"])
 @pytest.mark.parametrize("world,ne,nq,var_range,fit", [
     (2, 7, 5, (1, 3), "broadcast"),     # reference default var_range, ragged shards
     (3, 8, 4, (1, 8), "replicate"),     # full var_range, replicated factorisation
@@ -107,10 +134,10 @@ def _worker(rank, world, port, out, ne, nq, var_range, fit):
     (3, 10, 3, (4, 9), "broadcast"),    # variance rows in the middle: 3-piece shards
     (4, 9, 2, (1, 3), "replicate"),     # fewer variance rows than ranks
 ])
-def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit):
+def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit, kind):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, str(tmp_path), ne, nq, var_range, fit), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, port, str(tmp_path), ne, nq, var_range, fit, kind),
+             nprocs=world, join=True)
     kinds, hp, x, y, xe, xq = _problem(ne=ne, nq=nq)
     mu_o, var_o = O.split_predict(kinds, hp, x, y, xe, xq, var_range=var_range)
     for r in range(world):  # every rank holds the full result
@@ -119,6 +146,16 @@ def test_split_predict_distributed_gloo(tmp_path, world, ne, nq, var_range, fit)
         assert mu.shape == (ne, nq)
         np.testing.assert_allclose(mu, mu_o, rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(var, var_o, rtol=1e-12, atol=1e-14)
+    if kind == "shard":
+        # one predict_shard call per rank with rows, its buffers sized to the largest share
+        # (the all_gather's common size), not to the grid's ne rows
+        v_lo, v_hi = gd.var_rows(var_range, ne)
+        pieces = [gd.shard_pieces(ne, world, r, v_lo, v_hi) for r in range(world)]
+        emax = max(max(sum(b - a for a, b in p) for p in pieces), 1)
+        assert emax <= -(-ne // world) + 1
+        for r in range(world):
+            calls = eval(open(tmp_path / f"calls{r}.txt").read())
+            assert calls == ([(pieces[r], emax)] if pieces[r] else []), (r, calls)
 
 
 class FailingBackend(OracleBackend):
@@ -142,12 +179,18 @@ class FailingBackend(OracleBackend):
         return super().fit()
 
 
-def _fail_worker(rank, world, port, out, fit, fail, info, fail_rows=()):
+class FailingShardBackend(FailingBackend, ShardOracleBackend):
+    """FailingBackend behind the predict_shard interface (its predict_shard calls the
+    failing predict_rows)."""
+
+
+def _fail_worker(rank, world, port, out, fit, fail, info, fail_rows=(), kind="rows"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         kinds, hp, x, y, xe, xq = _problem(ne=5, nq=3)
-        be = FailingBackend(kinds, hp, x, y, fail=fail, info=info, fail_rows=fail_rows)
+        cls = FailingShardBackend if kind == "shard" else FailingBackend
+        be = cls(kinds, hp, x, y, fail=fail, info=info, fail_rows=fail_rows)
         try:
             gd.split_predict_distributed(None, _Cmap(xe, xq), backend=be, fit=fit)
             res = "ok"
@@ -300,12 +343,13 @@ def test_split_predict_distributed_hip_two_ranks(tmp_path, fit):
             np.testing.assert_allclose(np.load(tmp_path / f"var{r}_{it}.npy"), var1, rtol=1e-12, atol=1e-14)
 
 
+@pytest.mark.parametrize("kind", ["rows", "shard"])
 @pytest.mark.parametrize("fit", ["broadcast", "replicate"])
-def test_split_predict_distributed_shard_failure(tmp_path, fit):
-    """A shard that fails on one rank (rank 1's predict_rows raises) raises on EVERY rank
-    instead of leaving the others blocked in the all_gather."""
+def test_split_predict_distributed_shard_failure(tmp_path, fit, kind):
+    """A shard that fails on one rank (rank 1's predict_rows / predict_shard raises) raises on
+    EVERY rank instead of leaving the others blocked in the all_gather."""
     world = 3
-    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path), fit, (), 0, (1,)),
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path), fit, (), 0, (1,), kind),
              nprocs=world, join=True)
     res = [open(tmp_path / f"r{r}.txt").read() for r in range(world)]
     assert res[1].startswith("RuntimeError"), res
@@ -408,3 +452,55 @@ def test_split_predict_mgpu_broadcast_path_one_device(monkeypatch):
     mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 9))
     np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_split_predict_shard_compact_equals_rows():
+    """gpr_split_predict_shard (outputs sized to the shard: pieces' rows concatenated, mu with
+    leading dimension ldmu >= R) equals gpr_split_predict_rows' full-layout rows bit for bit,
+    for every rank's pieces of a 3-way split and with a padded leading dimension; ldmu < R is
+    refused."""
+    import ctypes
+    G = pytest.importorskip("gpr_amd")
+    from gpr_amd import core
+    from gpr_amd._lib import lib
+    kinds, hp, x, y, xe, xq = _problem(ne=23, nq=19, ns=600, d=4, seed=21)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    be = gd.HipSplitBackend(md)
+    U, wt = be.fit()
+    ctx = md.ctx
+    ctx.sync()
+    _, ne, nq = cm.shape
+    ka, nk = core._kinds_arr(md.covar)
+    _, hpp = core._hp_arr(md.params)
+    dxe, dxq = ctx.colmajor(cm.xe), ctx.colmajor(cm.xq)
+    v_lo, v_hi = 2, 17
+    for world in (1, 3):
+        for r in range(world):
+            pieces = gd.shard_pieces(ne, world, r, v_lo, v_hi)
+            R = sum(b - a for a, b in pieces)
+            flat = [v for p in pieces for v in p]
+            arr = (ctypes.c_int * max(len(flat), 1))(*flat)
+            mu_f, var_f = ctx.zeros(nq, ne), ctx.zeros(ne * nq)
+            assert lib.gpr_split_predict_rows(ctx.h, ka, nk, hpp, md.d, core._ptr(md.dx()), md.n,
+                                              core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
+                                              core._ptr(dxq), nq, arr, len(pieces), v_lo, v_hi,
+                                              core.EPS_DEFAULT, core._ptr(mu_f), core._ptr(var_f)) == 0
+            for ld in (R, R + 5):
+                mu_s, var_s = be.predict_shard(cm, U, wt, pieces, v_lo, v_hi, ld)
+                mf, vf, ms, vs = mu_f.cpu(), var_f.cpu(), mu_s.cpu(), var_s.cpu()
+                off = 0
+                for a, b in pieces:
+                    assert torch.equal(ms[:, off:off + b - a], mf[:, a:b])
+                    assert torch.equal(vs[off * nq:(off + b - a) * nq], vf[a * nq:b * nq])
+                    off += b - a
+                assert torch.all(ms[:, R:] == 0) and torch.all(vs[R * nq:] == 0)
+            if R > 1:
+                mu_s, var_s = ctx.zeros(nq, R), ctx.zeros(R * nq)
+                rc = lib.gpr_split_predict_shard(ctx.h, ka, nk, hpp, md.d, core._ptr(md.dx()), md.n,
+                                                 core._ptr(U), md.n, core._ptr(wt), core._ptr(dxe), ne,
+                                                 core._ptr(dxq), nq, arr, len(pieces), v_lo, v_hi,
+                                                 core.EPS_DEFAULT, core._ptr(mu_s), R - 1,
+                                                 core._ptr(var_s))
+                assert rc != 0

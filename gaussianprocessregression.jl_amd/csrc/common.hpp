@@ -89,6 +89,15 @@ struct gpr_ctx {
   int dag_fearly = 0;     // diagonal tasks right behind the tile they wait for (GPR_DAG_FEARLY;
                           // measured C2 -1..0 %, C4 -0.3 %, C3 +0.4 %: off)
   int dag_lag_built = -1;
+  // one-shot hook of the next whole-matrix factorisation launch (kglob 0, not a solve), called
+  // right after the kernel is enqueued with an event that completes once the launch's progress
+  // counters are reset (null if it could not be made): work ordered behind that event runs
+  // BESIDE the launch (mgpu.hip streams finished tile rows of U out to the other GPUs); cleared
+  // before the call
+  void (*dag_hook)(void* user, const double* dA, int n, int lda, const int* colprog, int nt,
+                   hipEvent_t counters_reset) = nullptr;
+  void* dag_hook_user = nullptr;
+  int dag_reserve_cu = 0;  // CUs the persistent grid leaves free for such concurrent work
   bool rhs_solved = false; // the last potrf_core solved its RhsSpec (not dropped by its block sizes)
   bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)
   int dag_gram = 1;       // K^{-1} += Z^T Z as gram tile tasks of the DAG launch (GPR_DAG_GRAM)

@@ -723,7 +723,21 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   // (re-read per launch: the timeout tests shorten it around one call)
   const char* sl = getenv("GPR_DAG_SPIN_LIMIT");
   a.spin_limit = sl ? std::max(1ll, atoll(sl)) : ctx->dag_spin_limit;
-  const int grid = std::min(ctx->dag_ntasks, ctx->ncu);
+  const int grid = std::min(ctx->dag_ntasks, std::max(1, ctx->ncu - ctx->dag_reserve_cu));
+  // the one-shot hook (common.hpp): an event between the counters' reset and the launch, the
+  // hook itself only after the launch is enqueued -- work it orders behind the event can then
+  // never sit ahead of the launch in a hardware queue that two streams share
+  auto hook = (ctx->dag_hook && !solve && !lower && kglob == 0) ? ctx->dag_hook : nullptr;
+  hipEvent_t hook_ev = nullptr;
+  if (hook) {
+    ctx->dag_hook = nullptr;
+    if (hipEventCreateWithFlags(&hook_ev, hipEventDisableTiming) != hipSuccess) hook_ev = nullptr;
+    if (hook_ev && hipEventRecord(hook_ev, st) != hipSuccess) {
+      hipEventDestroy(hook_ev);
+      hook_ev = nullptr;
+    }
+    (void)hipGetLastError();
+  }
   // factorisation n^3/3; U^{-T} B: n^2 per column, ~n^3/3 for a lower-triangular n x n B
   const double flops = (solve ? 0.0 : (double)n * n * n / 3.0) +
                        (lower ? (double)n * n * n / 3.0 : (double)n * n * (dB ? nrhs : 0)) +
@@ -738,6 +752,10 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
       potrf_dag_kernel<false><<<grid, 256, 0, st>>>(a);
     ctx->ls = ls;
     LAUNCH_CHECK(ctx);
+  }
+  if (hook) {
+    hook(ctx->dag_hook_user, dA, n, lda, ctx->dag_sync + 2, nt, hook_ev);
+    if (hook_ev) hipEventDestroy(hook_ev);
   }
   return 0;
 }

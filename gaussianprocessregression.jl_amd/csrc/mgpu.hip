@@ -4,9 +4,13 @@
 // The grid rows e of x_{e,q} = xe_e + xq_q are independent once the training factor U and the
 // weights wt = K^{-1} y exist:
 //   1. fit  -- GPR_MGPU_BROADCAST: device 0 fits (K, tile-DAG POTRF, wt) and RCCL broadcasts
-//              U's upper triangle packed by 128-column blocks (~4 N^2 bytes instead of 8 N^2)
-//              plus wt over xGMI; the receivers unpack it into their U and drop their cached
-//              block inverses (rebuilt from the received factor).
+//              U's upper triangle (~4 N^2 bytes instead of 8 N^2) plus wt over xGMI; the
+//              receivers unpack it into their U and drop their cached block inverses (rebuilt
+//              from the received factor).  The broadcast is STREAMED: U leaves in ~16 chunks of
+//              tile rows, each packed and broadcast as soon as the running tile-DAG launch has
+//              finalised its rows (a gate kernel polls the launch's progress counters; the
+//              launch leaves 8 CUs free for the gates, packs and RCCL kernels), so only the last
+//              chunk and wt trail the factorisation instead of the whole 4.3 GB (C5).
 //              GPR_MGPU_REPLICATE: every device fits for itself (no N^2 exchange: the fit is
 //              ~180 ms at ns = 32768 while the packed broadcast moves 4.3 GB).
 //   2. rows -- device i takes gpr_shard_pieces(ne, ngpu, i, var_lo, var_hi): an even share of
@@ -115,6 +119,79 @@ int launch_pack(gpr_ctx* ctx, double* U, int ldu, int n, double* P, bool pack) {
   return 0;
 }
 
+// ---- the streamed broadcast's layout: U's upper triangle by TILE ROWS ----------------------
+// Tile row i (rows [128 i, 128 i + m_i), m_i = min(128, n - 128 i), columns [128 i, n)) as an
+// m_i x (n - 128 i) column-major block, tile rows in order: the same elements as the
+// column-block packing, ordered so that a prefix of tile rows is a prefix of the buffer.  The
+// tile-DAG finalises U top-down by tile rows (left-looking, tickets by row), so a chunk of tile
+// rows can leave for the other GPUs while the factorisation is still running below it.
+__host__ __device__ inline size_t rows_base(int i, int n) {
+  return (size_t)PACK_NB * ((size_t)i * n - (size_t)PACK_NB * i * (i - 1) / 2);
+}
+
+// tile rows [r0, r1) of U <-> their slice of the row layout (PACK: U -> P).  Workgroup x = column
+// c of [128 r0, n): its rows [128 r0, min(128 r1, end of c's tile column)) are contiguous in U.
+template <bool PACK>
+__global__ __launch_bounds__(256) void rows_pack_kernel(double* __restrict__ U, size_t ldu, int n,
+                                                        int r0, int r1, double* __restrict__ P) {
+  const int c = PACK_NB * r0 + blockIdx.x;
+  const int rend = min(min(PACK_NB * r1, n), PACK_NB * (c / PACK_NB + 1));
+  for (int r = PACK_NB * r0 + blockIdx.y * 256 + threadIdx.x; r < rend; r += gridDim.y * 256) {
+    const int i = r / PACK_NB;
+    const int m = min(PACK_NB, n - PACK_NB * i);
+    double* p = P + rows_base(i, n) + (size_t)(c - PACK_NB * i) * m + (r - PACK_NB * i);
+    double* u = U + r + (size_t)c * ldu;
+    if (PACK)
+      *p = *u;
+    else
+      *u = *p;
+  }
+}
+
+// Waits until tile rows [r0, r1) of U are final in a running tile-DAG launch: colprog[j] (final
+// tiles at the top of tile column j, raised with sc1 stores after the tiles' sc1 stores drained)
+// >= min(r1, j + 1) for every j >= r0.  Bounded like the DAG's own waits: after `limit` polls
+// it flags *err and returns (the chunk then carries garbage and the host reports the error).
+__global__ __launch_bounds__(256) void rows_gate_kernel(const int* __restrict__ colprog, int nt,
+                                                        int r0, int r1, long long limit,
+                                                        int* __restrict__ err) {
+  long long spins = 0;
+  for (;;) {
+    int ok = 1;
+    for (int j = r0 + (int)threadIdx.x; j < nt; j += 256)
+      ok &= __hip_atomic_load(colprog + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+            min(r1, j + 1);
+    if (__syncthreads_and(ok)) break;
+    if (++spins > limit) {  // (spins is the same in every thread: a uniform exit)
+      if (threadIdx.x == 0) atomicExch(err, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+void launch_rows_pack(hipStream_t s, double* U, int ldu, int n, int r0, int r1, double* P,
+                      bool pack) {
+  const int rows = std::min(PACK_NB * r1, n) - PACK_NB * r0;
+  const dim3 grid(n - PACK_NB * r0, std::min(8, (rows + 255) / 256));
+  if (pack)
+    rows_pack_kernel<true><<<grid, 256, 0, s>>>(U, (size_t)ldu, n, r0, r1, P);
+  else
+    rows_pack_kernel<false><<<grid, 256, 0, s>>>(U, (size_t)ldu, n, r0, r1, P);
+}
+
+// chunk boundaries in tile rows: about equal bytes per chunk, at most `maxc` chunks
+std::vector<int> row_chunks(int n, int maxc) {
+  const int nt = (n + PACK_NB - 1) / PACK_NB;
+  const size_t total = packed_len(n);
+  const int C = std::max(1, std::min(maxc, nt));
+  std::vector<int> b{0};
+  for (int i = 1; i < nt; ++i)
+    if (rows_base(i, n) * C >= total * b.size() && (int)b.size() < C) b.push_back(i);
+  b.push_back(nt);
+  return b;
+}
+
 void shard_rows(int n, int world, int rank, int* lo, int* hi) {
   const int q = n / world, r = n % world;
   *lo = rank * q + std::min(rank, r);
@@ -132,10 +209,15 @@ struct gpr_mgpu {
   std::string err;
   struct Bufs {  // device buffers of one GPU, grown on demand
     double *x = nullptr, *y = nullptr, *xe = nullptr, *xq = nullptr, *U = nullptr, *wt = nullptr,
-           *mu = nullptr, *var = nullptr, *pk = nullptr;
-    size_t cx = 0, cy = 0, cxe = 0, cxq = 0, cU = 0, cwt = 0, cmu = 0, cvar = 0, cpk = 0;
+           *mu = nullptr, *var = nullptr, *pk = nullptr, *U2 = nullptr;
+    size_t cx = 0, cy = 0, cxe = 0, cxq = 0, cU = 0, cwt = 0, cmu = 0, cvar = 0, cpk = 0, cU2 = 0;
   };
   std::vector<Bufs> buf;
+  // device 0's stream for the streamed broadcast (gates, packs, RCCL), created after the
+  // context's five: a stream whose hardware queue is shared with the factorisation's stream
+  // (GPU_MAX_HW_QUEUES = 4) runs its work behind the launch, so everything goes on this one
+  hipStream_t sp = nullptr;
+  int* derr = nullptr;  // device 0: a gate timed out
 };
 
 namespace {
@@ -159,6 +241,56 @@ bool grow(double** p, size_t* cap, size_t n) {
   if (hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(double)) != hipSuccess) return false;
   *cap = n;
   return true;
+}
+
+// Device 0's side of the broadcast: chunk c = tile rows [rows[c], rows[c+1]) of U, packed into
+// its slice of pk (behind a gate on the DAG's progress counters when streamed), then broadcast
+// from that slice, all on stream sp.  Measured with one stream per role (pack / RCCL): the
+// second stream shared the launch's hardware queue and its work ran after the launch.  Called from the tile-DAG launch's hook (streamed:
+// the chunks run beside the factorisation, on the CUs its grid leaves free) or after the fit.
+struct StreamOut {
+  gpr_mgpu* h = nullptr;
+  int n = 0;
+  double *U = nullptr, *pk = nullptr, *U2 = nullptr;  // U2: self-broadcast receive buffer
+  std::vector<int> rows;
+  long long limit = 1ll << 27;  // gate polls (~minutes: a gate waits up to a whole fit)
+  bool fired = false;  // chunks enqueued by the hook, beside the DAG launch
+  int rc = 0;
+};
+
+// (dep: the event the chunks wait for -- the counters' reset, or the end of the fit)
+int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
+  gpr_mgpu* h = so->h;
+  auto& R = h->rccl;
+  int rc = 0;
+  if (hipStreamWaitEvent(h->sp, dep, 0) != hipSuccess) rc = GPR_E_HIP;
+  for (size_t c = 0; rc == 0 && c + 1 < so->rows.size(); ++c) {
+    const int r0 = so->rows[c], r1 = so->rows[c + 1];
+    double* slice = so->pk + rows_base(r0, so->n);
+    const size_t len = rows_base(r1 - 1, so->n) - rows_base(r0, so->n) +
+                       (size_t)std::min(PACK_NB, so->n - PACK_NB * (r1 - 1)) *
+                           (so->n - PACK_NB * (r1 - 1));
+    if (colprog) rows_gate_kernel<<<1, 256, 0, h->sp>>>(colprog, nt, r0, r1, so->limit, h->derr);
+    launch_rows_pack(h->sp, so->U, so->n, so->n, r0, r1, so->pk, true);
+    if (hipGetLastError() != hipSuccess ||
+        R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess) {
+      rc = GPR_E_HIP;
+      break;
+    }
+    if (so->U2) launch_rows_pack(h->sp, so->U2, so->n, so->n, r0, r1, so->pk, false);
+  }
+  return rc;
+}
+
+// The tile-DAG launch's hook on device 0 (called right after the launch is enqueued): the
+// gates, packs and broadcasts go on sp / sc behind the counters' reset, i.e. beside the launch.
+// A padded copy (other shapes) or a missing event: nothing here, the chunks follow the fit.
+void stream_out_hook(void* user, const double* dA, int n, int lda, const int* colprog, int nt,
+                     hipEvent_t counters_reset) {
+  auto* so = static_cast<StreamOut*>(user);
+  if (!counters_reset || dA != so->U || n != so->n || lda != so->n) return;
+  so->rc = enqueue_chunks(so, colprog, nt, counters_reset);
+  so->fired = true;
 }
 
 // run f(i) for every device on its own host thread (device i current), collect return codes
@@ -258,6 +390,28 @@ int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out) {
       return GPR_E_HIP;
     }
   }
+  if (hipSetDevice(h->dev[0]) != hipSuccess || hipMalloc((void**)&h->derr, sizeof(int)) != hipSuccess) {
+    gpr_mgpu_destroy(h);
+    return GPR_E_HIP;
+  }
+  {
+    // low priority (GPR_MGPU_SP=normal / high: the others).  Measured (profiles/
+    // r03_mgpu_stream_out_trace.txt): low, normal and high priority streams all ran the
+    // stream-out inside the launch's window; a CU-masked stream ran it after the launch.
+    const char* e = getenv("GPR_MGPU_SP");
+    const std::string kind = e ? e : "low";
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    const hipError_t r =
+        kind == "normal" ? hipStreamCreateWithFlags(&h->sp, hipStreamNonBlocking)
+                         : hipStreamCreateWithPriority(&h->sp, hipStreamNonBlocking,
+                                                       kind == "high" ? hi : lo);
+    if (r != hipSuccess) {
+      h->sp = nullptr;
+      gpr_mgpu_destroy(h);
+      return GPR_E_HIP;
+    }
+  }
   std::string err;
   if (!load_rccl(&h->rccl, &err)) {
     gpr_mgpu_destroy(h);
@@ -279,8 +433,12 @@ int gpr_mgpu_destroy(gpr_mgpu_t h) {
     if (hipSetDevice(h->dev[i]) != hipSuccess) continue;
     if (i < (int)h->comm.size() && h->comm[i] && h->rccl.CommDestroy) h->rccl.CommDestroy(h->comm[i]);
     auto& b = h->buf[i];
-    for (double* p : {b.x, b.y, b.xe, b.xq, b.U, b.wt, b.mu, b.var, b.pk})
+    for (double* p : {b.x, b.y, b.xe, b.xq, b.U, b.wt, b.mu, b.var, b.pk, b.U2})
       if (p) hipFree(p);
+    if (i == 0) {
+      if (h->sp) hipStreamDestroy(h->sp);
+      if (h->derr) hipFree(h->derr);
+    }
     if (h->ctx[i]) gpr_ctx_destroy(h->ctx[i]);
   }
   delete h;
@@ -316,7 +474,24 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     if (npc[i] < 0) return mg_err(h, GPR_E_ARG, "bad shard");
     for (int k = 0; k < npc[i]; ++k) rows[i] += pcs[i][2 * k + 1] - pcs[i][2 * k];
   }
-  // 1. inputs up, fit (device 0, or every device), device 0 packs U for the broadcast
+  // Broadcast protocol (every device runs it in full, whatever happens to the fit, so no
+  // receiver is left waiting in RCCL): chunks of tile rows of U in the row layout (about equal
+  // bytes, at most GPR_MGPU_CHUNKS = 16), then wt.  Streamed (default; GPR_MGPU_STREAM=0: after
+  // the fit): device 0's factorisation leaves GPR_MGPU_RESERVE_CU (8) CUs free and each chunk is
+  // packed and broadcast beside it as soon as its tile rows are final; the receivers unpack each
+  // chunk as it lands.  Only the last chunk and wt trail the factorisation.
+  const char* e_st = getenv("GPR_MGPU_STREAM");
+  const bool stream = !e_st || atoi(e_st) != 0;
+  const char* e_rs = getenv("GPR_MGPU_RESERVE_CU");
+  const int reserve = e_rs ? std::max(0, atoi(e_rs)) : 8;
+  const char* e_ch = getenv("GPR_MGPU_CHUNKS");
+  const int maxc = e_ch ? std::max(1, atoi(e_ch)) : 16;
+  StreamOut so;
+  so.h = h;
+  so.n = ns;
+  so.rows = row_chunks(ns, maxc);
+  // 0. buffers and inputs on every device (a failure here stops every device before the
+  //    broadcast protocol starts)
   auto rc = on_devices(h, [&](int i) -> int {
     gpr_ctx_t c = h->ctx[i];
     auto& b = h->buf[i];
@@ -325,17 +500,77 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
         !grow(&b.U, &b.cU, (size_t)ns * ns) || !grow(&b.wt, &b.cwt, ns) ||
         !grow(&b.mu, &b.cmu, (size_t)std::max(rows[i], 1) * nq) ||
         !grow(&b.var, &b.cvar, (size_t)std::max(rows[i], 1) * nq) ||
-        (bcast && !grow(&b.pk, &b.cpk, npk)))
+        (bcast && !grow(&b.pk, &b.cpk, npk)) ||
+        (bcast && self_bcast && !grow(&b.U2, &b.cU2, (size_t)ns * ns)))
       return set_err(c, GPR_E_NOMEM, "device %d: allocation failed", h->dev[i]);
     GPR_TRY(gpr_upload(c, b.x, X, sizeof(double) * d * ns));
     GPR_TRY(gpr_upload(c, b.y, y, sizeof(double) * ns));
     GPR_TRY(gpr_upload(c, b.xe, Xe, sizeof(double) * d * ne));
     GPR_TRY(gpr_upload(c, b.xq, Xq, sizeof(double) * d * nq));
-    if (!bcast || i == 0) {
+    if (i == 0) HIP_TRY(c, hipMemset(h->derr, 0, sizeof(int)));
+    return gpr_sync(c);
+  });
+  for (int i = 0; i < G; ++i)
+    if (rc[i] != 0)
+      return mg_err(h, rc[i] < 0 ? rc[i] : GPR_E_HIP, "device %d: %s", h->dev[i],
+                    gpr_last_error(h->ctx[i]));
+  // 1. device 0 (or every device) fits; device 0 sends U and wt, the receivers take them
+  rc = on_devices(h, [&](int i) -> int {
+    gpr_ctx_t c = h->ctx[i];
+    auto& b = h->buf[i];
+    if (!bcast) {
       const int r = gpr_fit(c, kinds, nk, hp, d, b.x, ns, b.y, 1, ns, eps, b.U, ns, b.wt, &finfo[i]);
       if (r != 0) return r;  // (> 0: the LAPACK info)
-      if (bcast) GPR_TRY(launch_pack(c, b.U, ns, ns, b.pk, true));
+      return gpr_sync(c);
     }
+    auto& R = h->rccl;
+    hipStream_t s = (hipStream_t)gpr_ctx_stream(c);
+    if (i > 0) {  // receiver: every chunk, unpacked as it lands, then wt
+      for (size_t k = 0; k + 1 < so.rows.size(); ++k) {
+        const int r0 = so.rows[k], r1 = so.rows[k + 1];
+        double* slice = b.pk + rows_base(r0, ns);
+        const size_t len = rows_base(r1 - 1, ns) - rows_base(r0, ns) +
+                           (size_t)std::min(PACK_NB, ns - PACK_NB * (r1 - 1)) * (ns - PACK_NB * (r1 - 1));
+        if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[i], s) != ncclSuccess)
+          return set_err(c, GPR_E_HIP, "RCCL broadcast of chunk %zu failed", k);
+        launch_rows_pack(s, b.U, ns, ns, r0, r1, b.pk, false);
+        HIP_TRY(c, hipGetLastError());
+      }
+      if (R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[i], s) != ncclSuccess)
+        return set_err(c, GPR_E_HIP, "RCCL broadcast of wt failed");
+      GPR_TRY(gpr_sync(c));
+      return gpr_forget_factor(c);  // the inverses of this buffer's old contents are stale
+    }
+    // device 0: fit with the hook armed, then whatever the hook did not send, then wt
+    so.U = b.U;
+    so.pk = b.pk;
+    so.U2 = self_bcast ? b.U2 : nullptr;
+    if (stream) {
+      c->dag_hook = stream_out_hook;
+      c->dag_hook_user = &so;
+      c->dag_reserve_cu = reserve;
+    }
+    const int r = gpr_fit(c, kinds, nk, hp, d, b.x, ns, b.y, 1, ns, eps, b.U, ns, b.wt, &finfo[0]);
+    c->dag_hook = nullptr;
+    c->dag_reserve_cu = 0;
+    (void)hipGetLastError();  // (a failed fit must not stop the protocol below)
+    int prc = so.fired ? so.rc : 0;
+    hipEvent_t fit_done = nullptr;  // wt (and, unless streamed, U) leave after the fit
+    if (hipEventCreateWithFlags(&fit_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(fit_done, s) != hipSuccess)
+      prc = GPR_E_HIP;
+    if (prc == 0 && !so.fired) prc = enqueue_chunks(&so, nullptr, 0, fit_done);
+    if (prc == 0 && hipStreamWaitEvent(h->sp, fit_done, 0) != hipSuccess) prc = GPR_E_HIP;
+    if (prc == 0 && R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess)
+      prc = GPR_E_HIP;
+    if (fit_done) hipEventDestroy(fit_done);
+    if (hipStreamSynchronize(h->sp) != hipSuccess) prc = GPR_E_HIP;
+    if (r != 0) return r;
+    if (prc != 0) return set_err(c, GPR_E_HIP, "device 0: streaming U / wt out failed");
+    int herr = 0;
+    HIP_TRY(c, hipMemcpy(&herr, h->derr, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr) return set_err(c, GPR_E_HIP, "device 0: a tile-row gate timed out");
+    if (self_bcast) GPR_TRY(gpr_forget_factor(c));
     return gpr_sync(c);
   });
   for (int i = 0; i < G; ++i) {
@@ -347,33 +582,15 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     if (rc[i] < 0)
       return mg_err(h, rc[i], "device %d: %s", h->dev[i], gpr_last_error(h->ctx[i]));
   }
-  // 2. broadcast the packed factor and wt from device 0 (one RCCL group over all devices)
-  if (bcast) {
-    auto& R = h->rccl;
-    ncclResult_t r = R.GroupStart();
-    for (int i = 0; i < G && r == ncclSuccess; ++i) {
-      hipStream_t s = (hipStream_t)gpr_ctx_stream(h->ctx[i]);
-      r = R.Broadcast(h->buf[i].pk, h->buf[i].pk, npk, ncclDouble, 0, h->comm[i], s);
-      if (r == ncclSuccess)
-        r = R.Broadcast(h->buf[i].wt, h->buf[i].wt, ns, ncclDouble, 0, h->comm[i], s);
-    }
-    const ncclResult_t r2 = R.GroupEnd();
-    if (r != ncclSuccess || r2 != ncclSuccess)
-      return mg_err(h, GPR_E_HIP, "RCCL broadcast: %s",
-                    R.GetErrorString(r != ncclSuccess ? r : r2));
-  }
-  // 3. receivers unpack; every device predicts its rows and copies them into the host arrays
+  // 2. every device predicts its rows and copies them into the host arrays
   rc = on_devices(h, [&](int i) -> int {
     gpr_ctx_t c = h->ctx[i];
     auto& b = h->buf[i];
-    if (bcast && (i > 0 || self_bcast)) {
-      GPR_TRY(launch_pack(c, b.U, ns, ns, b.pk, false));
-      GPR_TRY(gpr_forget_factor(c));  // the inverses of this buffer's old contents are stale
-    }
+    const double* U = (bcast && self_bcast) ? b.U2 : b.U;  // (self: the received copy)
     const int* pieces = pcs[i].data();
     const int np = npc[i], R = std::max(rows[i], 1);
     // the shard's rows only (compact: piece k's rows at off_k, mu leading dimension R)
-    GPR_TRY(split_predict_pieces(c, kinds, nk, hp, d, b.x, ns, b.U, ns, b.wt, b.xe, ne, b.xq, nq,
+    GPR_TRY(split_predict_pieces(c, kinds, nk, hp, d, b.x, ns, U, ns, b.wt, b.xe, ne, b.xq, nq,
                                  pieces, np, var_lo, var_hi, eps, b.mu, R, b.var, true));
     hipStream_t s = (hipStream_t)gpr_ctx_stream(c);
     for (int k = 0, off = 0; k < np; off += pieces[2 * k + 1] - pieces[2 * k], ++k) {

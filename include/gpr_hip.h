@@ -328,7 +328,12 @@ const char* gpr_mgpu_last_error(gpr_mgpu_t h);
  * fit_mode GPR_MGPU_BROADCAST / GPR_MGPU_REPLICATE.  Device i computes the rows
  * gpr_shard_pieces(ne, ngpu, i, var_lo, var_hi) and copies them into mu / var itself.
  * Returns > 0 (and *info) when K is not positive definite.  With ngpu = 1 the result equals
- * gpr_fit + gpr_split_predict on that device bit for bit. */
+ * gpr_fit + gpr_split_predict on that device bit for bit.
+ * Broadcast mode streams U out while device 0 factors it: chunks of 128-row tile rows
+ * (GPR_MGPU_CHUNKS, default 16, about equal bytes) are packed and broadcast as soon as the
+ * tile-DAG launch has finalised them, on a stream of their own and the GPR_MGPU_RESERVE_CU
+ * (default 8) CUs the launch leaves free; the receivers unpack each chunk as it lands.
+ * GPR_MGPU_STREAM=0 sends the same chunks after the fit instead. */
 int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double* hp, int d,
                            const double* X, int ns, const double* y, const double* Xe, int ne,
                            const double* Xq, int nq, int var_lo, int var_hi, double eps,

@@ -434,19 +434,32 @@ def test_split_predict_mgpu_one_device(fit):
 
 
 @pytest.mark.gpu
-def test_split_predict_mgpu_broadcast_path_one_device(monkeypatch):
+@pytest.mark.parametrize("ns,stream,chunks", [
+    (1504, "1", "16"),   # streamed beside the tile-DAG launch, ragged last tile row (96 rows)
+    (1504, "1", "1"),    # one chunk: everything after the last tile row
+    (4096, "1", "5"),    # 32 tile rows in 5 chunks
+    (1504, "0", "3"),    # chunks after the fit (GPR_MGPU_STREAM=0)
+    (1500, "1", "16"),   # n % 16 != 0: the padded factorisation declines the hook -> after the fit
+])
+def test_split_predict_mgpu_broadcast_path_one_device(monkeypatch, ns, stream, chunks):
     """The broadcast path of gpr_split_predict_mgpu on the one-GPU box (GPR_MGPU_SELF_BCAST):
-    device 0 packs U, runs the 1-rank RCCL broadcast of the packed factor and wt, unpacks into
-    U as a receiver does and drops its cached block inverses; the result equals the
-    single-device split predict up to the rebuilt inverses' rounding (rtol 1e-12)."""
+    device 0 factors with the hook armed (8 CUs left free), packs each chunk of tile rows as
+    soon as the tile-DAG's progress counters show it final, runs the 1-rank RCCL broadcast of
+    the chunk, unpacks it into a second buffer as a receiver does and predicts from that copy
+    with rebuilt block inverses; the result equals the single-device split predict up to the
+    rebuilt inverses' rounding (rtol 1e-12) -- a chunk packed before its rows were final would
+    differ at O(1)."""
     G = pytest.importorskip("gpr_amd")
     monkeypatch.setenv("GPR_MGPU_SELF_BCAST", "1")
-    kinds, hp, x, y, xe, xq = _problem(ne=9, nq=33, ns=1500, d=5, seed=12)
+    monkeypatch.setenv("GPR_MGPU_STREAM", stream)
+    monkeypatch.setenv("GPR_MGPU_CHUNKS", chunks)
+    kinds, hp, x, y, xe, xq = _problem(ne=9, nq=33, ns=ns, d=5, seed=12)
     md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
     cm = G.Cmap("+", xe, xq)
     mg = gd.MultiGPU([0])
     try:
-        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 9), fit="broadcast")
+        for _ in range(2):  # (the second call re-uses every buffer)
+            mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 9), fit="broadcast")
     finally:
         mg.close()
     mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 9))

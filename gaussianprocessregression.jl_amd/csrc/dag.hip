@@ -88,7 +88,7 @@ constexpr int DRPD = 64 / DNCH;             // rows per wave-wide 1-KB DMA
 constexpr int DNDMA = DT / (4 * DRPD);      // DMA instructions per wave per operand
 constexpr int DVM = 2 * DNDMA;              // vmcnt increments per stage
 constexpr int DNP = DTK / 8;                // fragment blocks (2 k-steps each) per stage
-static_assert(D2_PK + 4 * D2_PB + 2 <= DLDS, "diagonal block must fit in the stage buffers");
+static_assert(D2_LDS_DOUBLES <= DLDS, "diagonal block must fit in the stage buffers");
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 

@@ -16,6 +16,7 @@ namespace {
 constexpr int DIAG_THREADS = 256;
 
 typedef double d4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -69,6 +70,10 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 constexpr int D2_NB = 128;
 constexpr int D2_PK = D2_NB * (D2_NB + 1) / 2;  // packed 128x128 upper (66 KB)
 constexpr int D2_PB = 32 * 33 / 2;              // packed 32x32 upper
+// the factor's LDS: S (D2_PK), Xd (4 D2_PB), the fail flag (2 doubles' room), then per wave a
+// 64-double pivot-row buffer (16-B aligned)
+constexpr int D2_PIV = D2_PK + 4 * D2_PB + 2;
+constexpr int D2_LDS_DOUBLES = D2_PIV + 4 * 64;
 
 // column half (J, jh) of W = U^-1 (see above); S = U packed upper (128), Xd = packed diag inverses
 template <int J, bool SC1>
@@ -185,6 +190,14 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
 #pragma unroll
       for (int r = 0; r < 32; ++r) x[r] = il ? (r == q ? 1.0 : 0.0) : ((dl && r > lane) ? 0.0 : x[r]);
       int bad = 0;
+#ifndef D2_READLANE_ROWS
+      // the pivot row through this wave's own LDS buffer: every lane writes its x[j] (lanes
+      // 0-31 hold row j of the band's diagonal block), then every lane reads the entries it
+      // needs as 16-B broadcasts -- one ds_write + (31 - j) / 2 ds_reads per step instead of
+      // two v_readlane per entry.  A wave's LDS operations complete in order, so the next
+      // step's write cannot overtake this step's reads; no other wave touches the buffer.
+      double* pivb = S + D2_PIV + 64 * wv;
+#endif
 #pragma unroll
       for (int j = 0; j < 32; ++j) {
         const double piv = readlane_d(x[j], j);
@@ -193,6 +206,32 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
         const double u = piv * ri;
         const double xs = x[j] * ri;
         x[j] = dl ? (lane == j ? u : (lane < j ? x[j] : xs)) : xs;
+#ifndef D2_READLANE_ROWS
+        if (j < 31) {  // (a condition, not a break: the loop must stay fully unrolled)
+        pivb[lane] = x[j];
+        asm volatile("" ::: "memory");  // (compiler order only: the LDS unit keeps the wave's)
+        // reads issued in groups of 8 pairs before the group's FMAs (left to itself the
+        // compiler put every read in the same registers with a wait behind each)
+#pragma unroll
+        for (int g0 = (j + 1) & ~1; g0 < 32; g0 += 16) {
+          d2v r2[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (g0 + 2 * t < 32) r2[t] = *reinterpret_cast<const d2v*>(pivb + g0 + 2 * t);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int i0 = g0 + 2 * t;
+            if (i0 < 32) {
+              if (i0 > j) x[i0] = fma(-r2[t][0], x[j], x[i0]);
+              x[i0 + 1] = fma(-r2[t][1], x[j], x[i0 + 1]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("" ::: "memory");
+        }
+#else
         // row j to every lane in groups of 8: the readlanes of a group are issued back to
         // back (their latency overlaps), then the group's FMAs; sched barriers keep the
         // compiler from hoisting a whole step's readlanes (SGPR pressure)
@@ -208,6 +247,7 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
             if (i0 + t < 32) x[i0 + t] = fma(-u8[t], x[j], x[i0 + t]);
           __builtin_amdgcn_sched_barrier(0);
         }
+#endif
       }
       if (dl) {
         if (wv == 0) {

@@ -367,7 +367,7 @@ __global__ __launch_bounds__(DIAG_THREADS, 2) void diag_block_kernel(double* __r
 // compiler sees that two workgroups cannot share a CU, drops the 2-per-CU register target and
 // allocates ~310 registers per wave, and the kernel would no longer fit beside a trailing-
 // update workgroup (224 registers per wave).
-constexpr size_t DIAG2_LDS = sizeof(double) * (D2_PK + 4 * D2_PB) + 16;
+constexpr size_t DIAG2_LDS = sizeof(double) * D2_LDS_DOUBLES;
 __global__ __launch_bounds__(DIAG_THREADS, 2) void diag2_kernel(double* __restrict__ A, size_t lda,
                                                                 int n, int kglob,
                                                                 int* __restrict__ info,

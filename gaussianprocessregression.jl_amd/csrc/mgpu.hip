@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void rows_gate_kernel(const int* __restrict__ 
                                                         int* __restrict__ err) {
   long long spins = 0;
   for (;;) {
-    int ok = 1;
+    int ok = limit > 0;  // (limit 0: give up at once)
     for (int j = r0 + (int)threadIdx.x; j < nt; j += 256)
       ok &= __hip_atomic_load(colprog + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
             min(r1, j + 1);
@@ -490,6 +490,9 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   so.h = h;
   so.n = ns;
   so.rows = row_chunks(ns, maxc);
+  // (tests: GPR_MGPU_GATE_LIMIT=0 makes every gate give up at once -- the error path whatever
+  // the factorisation's progress)
+  if (const char* e = getenv("GPR_MGPU_GATE_LIMIT")) so.limit = std::max(0ll, atoll(e));
   // 0. buffers and inputs on every device (a failure here stops every device before the
   //    broadcast protocol starts)
   auto rc = on_devices(h, [&](int i) -> int {

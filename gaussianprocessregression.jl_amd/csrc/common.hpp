@@ -112,6 +112,10 @@ struct gpr_ctx {
   size_t padA_cap = 0;
   double* dpadB = nullptr;
   size_t padB_cap = 0;
+  // rocSOLVER (dlopen'd, gpr_integrate_noise's eigendecomposition): a rocBLAS handle on this
+  // context's stream, created on first use; rb_destroy releases it
+  void* rb_handle = nullptr;
+  int (*rb_destroy)(void*) = nullptr;
   int ncu = 0;
   std::vector<hipEvent_t> sync_events;
   size_t ev_next = 0;

@@ -246,6 +246,7 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dag_sync) hipFree(ctx->dag_sync);
   if (ctx->dpadA) hipFree(ctx->dpadA);
   if (ctx->dpadB) hipFree(ctx->dpadB);
+  if (ctx->rb_handle && ctx->rb_destroy) ctx->rb_destroy(ctx->rb_handle);
   if (ctx->winv) hipFree(ctx->winv);
   if (ctx->dinfo) hipFree(ctx->dinfo);
   if (ctx->dexptab) hipFree(ctx->dexptab);

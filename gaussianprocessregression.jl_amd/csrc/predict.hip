@@ -16,7 +16,11 @@
 #include <algorithm>
 #include <cmath>
 #include <functional>
+#include <mutex>
 #include <thread>
+
+#include <dlfcn.h>
+#include <rocsolver/rocsolver.h>
 
 #include "common.hpp"
 
@@ -701,6 +705,135 @@ static int integ_noise_cols(gpr_ctx* c, const double* K, int ldk, int n, const d
   return 0;
 }
 
+// ---- rocSOLVER, dlopen'd (the process's own librocsolver.so.0 if loaded -- torch carries
+// one -- else the system's; no link-time dependency), for the eigendecomposition of K
+struct RocsolverApi {
+  bool tried = false, ok = false;
+  decltype(&rocblas_create_handle) create = nullptr;
+  decltype(&rocblas_destroy_handle) destroy = nullptr;
+  decltype(&rocblas_set_stream) set_stream = nullptr;
+  decltype(&rocsolver_dsyevd) dsyevd = nullptr;
+};
+static RocsolverApi g_rs;
+static std::mutex g_rs_mu;
+
+static bool load_rocsolver() {
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  if (g_rs.tried) return g_rs.ok;
+  g_rs.tried = true;
+  void* h = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return false;
+  // (dlsym on the rocSOLVER handle also searches its dependency, the rocBLAS it was built on)
+  g_rs.create = (decltype(g_rs.create))dlsym(h, "rocblas_create_handle");
+  g_rs.destroy = (decltype(g_rs.destroy))dlsym(h, "rocblas_destroy_handle");
+  g_rs.set_stream = (decltype(g_rs.set_stream))dlsym(h, "rocblas_set_stream");
+  g_rs.dsyevd = (decltype(g_rs.dsyevd))dlsym(h, "rocsolver_dsyevd");
+  g_rs.ok = g_rs.create && g_rs.destroy && g_rs.set_stream && g_rs.dsyevd;
+  return g_rs.ok;
+}
+
+static int rb_destroy_fn(void* hdl) {
+  return g_rs.destroy ? (int)g_rs.destroy((rocblas_handle)hdl) : 0;
+}
+
+// out[2j] = Iout_j = sum_i T[i, j] c_i / (lambda_i + noise_j), out[2j+1] = var_j = k2 - sum_i
+// c_i^2 / (lambda_i + noise_j), c = T[:, ny] = P^T k1  (src/integrate.jl:81-87,89-104,149-162:
+// Iout_j = wt_j' k1 with wt_j = P (lambda + noise_j)^-1 P' y_j, the same sum reassociated)
+__global__ __launch_bounds__(256) void quad_diag_update_kernel(const double* __restrict__ T, int n,
+                                                               int ny, const double* __restrict__ lam,
+                                                               const double* __restrict__ noise,
+                                                               double k2, double* __restrict__ out) {
+  __shared__ double red[2][256];
+  const int j = blockIdx.x;
+  const double* tj = T + (size_t)j * n;
+  const double* c = T + (size_t)ny * n;
+  const double e = noise[j];
+  double si = 0.0, sv = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const double r = 1.0 / (lam[i] + e);
+    si += tj[i] * c[i] * r;
+    sv += c[i] * c[i] * r;
+  }
+  red[0][threadIdx.x] = si;
+  red[1][threadIdx.x] = sv;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[2 * j] = red[0][0];
+    out[2 * j + 1] = k2 - red[1][0];
+  }
+}
+
+// gpr_integrate_noise by one symmetric eigendecomposition of K (in place: K <- P), as the
+// reference: T = P^T [Y | k1] on the MFMA GEMM, then one diagonal update per column.  Returns 1
+// (nothing done) when rocSOLVER cannot be loaded.
+static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k2, int n,
+                             const double* dy, int ny, int ldy, const double* noise, double* Iout,
+                             double* var) {
+  if (!load_rocsolver()) return 1;
+  if (!ctx->rb_handle) {
+    rocblas_handle hb = nullptr;
+    if (g_rs.create(&hb) != rocblas_status_success)
+      return set_err(ctx, GPR_E_HIP, "rocblas_create_handle failed");
+    ctx->rb_handle = hb;
+    ctx->rb_destroy = rb_destroy_fn;
+  }
+  rocblas_handle hb = (rocblas_handle)ctx->rb_handle;
+  if (g_rs.set_stream(hb, ctx->stream) != rocblas_status_success)
+    return set_err(ctx, GPR_E_HIP, "rocblas_set_stream failed");
+  // workspace (dbig): B = [Y | k1] (n x (ny+1)), T (n x (ny+1)), lambda, E, noise, out, info
+  const size_t nb = (size_t)n * (ny + 1);
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, 2 * nb + 2 * (size_t)n + 3 * (size_t)ny + 1));
+  double* B = ctx->dbig;
+  double* T = B + nb;
+  double* lam = T + nb;
+  double* E = lam + n;
+  double* dnoise = E + n;
+  double* out = dnoise + ny;
+  int* dinfo = reinterpret_cast<int*>(out + 2 * (size_t)ny);
+  HIP_TRY(ctx, hipMemcpy2DAsync(B, sizeof(double) * n, dy, sizeof(double) * ldy,
+                                sizeof(double) * n, ny, hipMemcpyDeviceToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(B + (size_t)ny * n, k1, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise, sizeof(double) * ny, hipMemcpyHostToDevice,
+                              ctx->stream));
+  // LAPACK.syevr!(ws, 'V', 'A', 'U', kxx, ...) -> eigenvalues ascending, eigenvectors in K
+  if (g_rs.dsyevd(hb, rocblas_evect_original, rocblas_fill_upper, n, K, n, lam, E, dinfo) !=
+      rocblas_status_success)
+    return set_err(ctx, GPR_E_HIP, "rocsolver_dsyevd failed");
+  int hinfo = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  // T = P^T B
+  GemmArgs g{};
+  g.P = K; g.ldp = n;
+  g.Q = B; g.ldq = n;
+  g.C = T; g.ldc = n;
+  g.M = n; g.N = ny + 1; g.K = n;
+  g.alpha = 1.0; g.beta = 0.0;
+  GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+  quad_diag_update_kernel<<<ny, 256, 0, ctx->stream>>>(T, n, ny, lam, dnoise, k2, out);
+  LAUNCH_CHECK(ctx);
+  std::vector<double> h(2 * (size_t)ny);
+  HIP_TRY(ctx, hipMemcpyAsync(h.data(), out, sizeof(double) * 2 * ny, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (hinfo != 0)
+    return set_err(ctx, GPR_E_HIP, "rocsolver_dsyevd did not converge (info %d)", hinfo);
+  for (int j = 0; j < ny; ++j) {
+    Iout[j] = h[2 * j];
+    var[j] = h[2 * j + 1];
+  }
+  return 0;
+}
+
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                         const double* dX, int n, const double* dy, int ny, int ldy,
                         const double* a, const double* b, const double* noise, double eps,
@@ -717,6 +850,14 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, K, n));
   double k2 = 0.0;
   GPR_TRY(gpr_antideriv_se(ctx, d, hp, dX, n, a, b, k1, &k2));
+  // the reference's path: K = P diag(lambda) P^T once (LAPACK.syevr!, :75), then per column
+  // j only diagonal updates (inverse_diagonal_update!, :81-104).  GPR_QUAD_EIGEN=0, or no
+  // loadable rocSOLVER: K + noise_j I factored per column (PD shifts only)
+  const char* qe = getenv("GPR_QUAD_EIGEN");
+  if (!qe || atoi(qe) != 0) {
+    const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var);
+    if (rc != 1) return rc;  // (1: rocSOLVER unavailable)
+  }
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);
   if (n > 8192) nsub = 1;
   nsub = cap_children_by_memory(nsub, ((size_t)n * n + 2 * (size_t)n + 2 * (size_t)ny) * 8);

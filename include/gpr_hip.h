@@ -236,12 +236,14 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
 
 /* integrate(md, hp, a, b; sample_noise = noise::Vector) (src/integrate.jl:71-100,149-162):
  * per column j of y (ny columns, noise[j] host), Iout[j] = k1' (K + noise_j I)^{-1} y_j and
- * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  The reference diagonalises K once (LAPACK
- * syevr) and applies (Lambda + noise_j)^{-1}; here each shifted matrix is factored by the
- * MFMA POTRF (same quantities; independent columns run on concurrent child contexts).
- * Returns info > 0 if some K + noise_j I is not positive definite.  Divergence from the
- * reference (which diagonalises K and never throws): for noise_j <= -lambda_min(K) the
- * reference returns an indefinite solve, this returns info > 0 (PosDefException). */
+ * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  As the reference: K = P Lambda P' once (the
+ * reference's LAPACK syevr; here rocSOLVER dsyevd, dlopen'd -- the process's librocsolver.so.0
+ * if loaded, else the system's), T = P' [y | k1] on the MFMA GEMM, then Iout[j] = sum_i
+ * T_ij (P'k1)_i / (lambda_i + noise_j) and var[j] = k2 - sum_i (P'k1)_i^2 / (lambda_i +
+ * noise_j): any shift, no factorisation, never info > 0 (an indefinite K + noise_j I gives
+ * the reference's indefinite solve).  Without a loadable rocSOLVER, or with GPR_QUAD_EIGEN=0,
+ * each K + noise_j I is factored by the MFMA POTRF instead (same quantities for positive
+ * definite shifts; returns info > 0 -- PosDefException -- for the others). */
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                         const double* dX, int n, const double* dy, int ny, int ldy,
                         const double* a, const double* b, const double* noise, double eps,

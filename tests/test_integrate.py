@@ -140,11 +140,12 @@ def test_integrate_sample_noise_vs_oracle(name, dim, n, ne):
 
 
 @pytest.mark.gpu
-def test_integrate_sample_noise_negative():
-    """Boundary of the documented divergence: a negative noise that keeps
-    K + noise I positive definite matches the oracle's eigen path (src/integrate.jl:71-100);
-    one below -lambda_min raises PosDefException where the reference's eigen path would
-    return an indefinite solve."""
+def test_integrate_sample_noise_negative(monkeypatch):
+    """Negative sample noise, as the reference's eigen path takes it (src/integrate.jl:71-100:
+    K = P Lambda P' once, (Lambda + noise_j)^-1 per column, never a factorisation): a shift
+    that keeps K + noise I positive definite and one that makes it negative definite both
+    match the oracle's eigen path -- no PosDefException.  With GPR_QUAD_EIGEN=0 (per-column
+    factorisations, the fallback when rocSOLVER cannot be loaded) the second raises."""
     dim, n = 3, 200
     kinds = [O.SE, O.WN]
     rng = np.random.default_rng(5)
@@ -153,14 +154,20 @@ def test_integrate_sample_noise_negative():
     hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)   # lambda_min(K) >= 0.05^2
     md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y)
     a, b = np.zeros(dim), np.ones(dim)
-    lam_min = np.linalg.eigvalsh(O.kernel(kinds, hp, x)).min()
-    noise = np.array([-0.5 * lam_min, 0.0])
+    lam = np.linalg.eigvalsh(O.kernel(kinds, hp, x))
+    noise = np.array([-0.5 * lam.min(), 0.0])
     I, v = G.integrate(md, a, b, sample_noise=noise)
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
     np.testing.assert_allclose(I, Io, rtol=1e-7)
     np.testing.assert_allclose(v, vo, rtol=1e-6, atol=1e-10 * O.antideriv2_se(hp, a, b))
+    neg = np.array([1e-3, -1.5 * lam.max()])   # K + noise I negative definite, well away from 0
+    I, v = G.integrate(md, a, b, sample_noise=neg)
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, neg)
+    np.testing.assert_allclose(I, Io, rtol=1e-8)
+    np.testing.assert_allclose(v, vo, rtol=1e-8)
+    monkeypatch.setenv("GPR_QUAD_EIGEN", "0")
     with pytest.raises(G.PosDefException):
-        G.integrate(md, a, b, sample_noise=np.array([1e-3, -2.0 * lam_min - 1.0]))
+        G.integrate(md, a, b, sample_noise=neg)
 
 
 @pytest.mark.gpu

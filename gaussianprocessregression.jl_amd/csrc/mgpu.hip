@@ -243,11 +243,18 @@ bool grow(double** p, size_t* cap, size_t n) {
   return true;
 }
 
+// elements of chunk [r0, r1) of tile rows in the row layout
+size_t chunk_len(int r0, int r1, int n) {
+  const int m = std::min(PACK_NB, n - PACK_NB * (r1 - 1));  // rows of the last tile row
+  return rows_base(r1 - 1, n) - rows_base(r0, n) + (size_t)m * (n - PACK_NB * (r1 - 1));
+}
+
 // Device 0's side of the broadcast: chunk c = tile rows [rows[c], rows[c+1]) of U, packed into
 // its slice of pk (behind a gate on the DAG's progress counters when streamed), then broadcast
-// from that slice, all on stream sp.  Measured with one stream per role (pack / RCCL): the
-// second stream shared the launch's hardware queue and its work ran after the launch.  Called from the tile-DAG launch's hook (streamed:
-// the chunks run beside the factorisation, on the CUs its grid leaves free) or after the fit.
+// from that slice, all on stream sp (measured with one stream per role, pack and RCCL: the
+// second stream shared the launch's hardware queue and its work ran after the launch).  Called
+// from the tile-DAG launch's hook (streamed: the chunks run beside the factorisation, on the
+// CUs its grid leaves free) or after the fit.
 struct StreamOut {
   gpr_mgpu* h = nullptr;
   int n = 0;
@@ -267,9 +274,7 @@ int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
   for (size_t c = 0; rc == 0 && c + 1 < so->rows.size(); ++c) {
     const int r0 = so->rows[c], r1 = so->rows[c + 1];
     double* slice = so->pk + rows_base(r0, so->n);
-    const size_t len = rows_base(r1 - 1, so->n) - rows_base(r0, so->n) +
-                       (size_t)std::min(PACK_NB, so->n - PACK_NB * (r1 - 1)) *
-                           (so->n - PACK_NB * (r1 - 1));
+    const size_t len = chunk_len(r0, r1, so->n);
     if (colprog) rows_gate_kernel<<<1, 256, 0, h->sp>>>(colprog, nt, r0, r1, so->limit, h->derr);
     launch_rows_pack(h->sp, so->U, so->n, so->n, r0, r1, so->pk, true);
     if (hipGetLastError() != hipSuccess ||
@@ -283,7 +288,7 @@ int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
 }
 
 // The tile-DAG launch's hook on device 0 (called right after the launch is enqueued): the
-// gates, packs and broadcasts go on sp / sc behind the counters' reset, i.e. beside the launch.
+// gates, packs and broadcasts go on sp behind the counters' reset, i.e. beside the launch.
 // A padded copy (other shapes) or a missing event: nothing here, the chunks follow the fit.
 void stream_out_hook(void* user, const double* dA, int n, int lda, const int* colprog, int nt,
                      hipEvent_t counters_reset) {
@@ -532,8 +537,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
       for (size_t k = 0; k + 1 < so.rows.size(); ++k) {
         const int r0 = so.rows[k], r1 = so.rows[k + 1];
         double* slice = b.pk + rows_base(r0, ns);
-        const size_t len = rows_base(r1 - 1, ns) - rows_base(r0, ns) +
-                           (size_t)std::min(PACK_NB, ns - PACK_NB * (r1 - 1)) * (ns - PACK_NB * (r1 - 1));
+        const size_t len = chunk_len(r0, r1, ns);
         if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[i], s) != ncclSuccess)
           return set_err(c, GPR_E_HIP, "RCCL broadcast of chunk %zu failed", k);
         launch_rows_pack(s, b.U, ns, ns, r0, r1, b.pk, false);

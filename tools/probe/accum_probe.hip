@@ -391,6 +391,8 @@ int main(int argc, char** argv) {
     case 4: run_priv<8, 4>(M, ld, ncolblk, K, reps, mode, out, cus); break;   // 128 KB
     case 5: run_priv<8, 5>(M, ld, ncolblk, K, reps, mode, out, cus); break;   // 160 KB
     case 6: run_priv<16, 2>(M, ld, ncolblk, K, reps, mode, out, cus); break;  // 128 KB
+    case 7: run<1, 8, 4, true>(M, ld, ncolblk, K, reps, mode, out, cus); break;   // 128 x 128, 2 waves/SIMD (32 x 64 each)
+    case 8: run<1, 8, 4, false>(M, ld, ncolblk, K, reps, mode, out, cus); break;
   }
   return 0;
 }

@@ -313,7 +313,11 @@ __device__ __attribute__((noinline)) int dag_factor(double* S, double* T, size_t
 // kernel only (out of line, the calls' register saves slowed every task by ~2 %; inlined
 // into the one kernel, its second copy of the pipeline cost the plain factorisation ~0.3 %)
 __device__ __forceinline__ void dag_gram_task(const DagArgs& a, int i_, int j_,
-                                                        double* lds, int* s_wait) {
+                                                        double* lds, int* s_wait,
+                                                        unsigned long long& p_wait,
+                                                        unsigned long long& p_acc) {
+  (void)p_wait;
+  (void)p_acc;
   // (values steering the loop around the barriers are readfirstlane'd: see the kernel)
   const int i = __builtin_amdgcn_readfirstlane(i_), j = __builtin_amdgcn_readfirstlane(j_);
   const int n = __builtin_amdgcn_readfirstlane(a.n), nt = __builtin_amdgcn_readfirstlane(a.nt);
@@ -332,10 +336,11 @@ __device__ __forceinline__ void dag_gram_task(const DagArgs& a, int i_, int j_,
   const double* Qcol = a.B + (size_t)j * DT * a.ldb;
   int done = j;
   while (done < nt) {
-    const int r = dag_wait(rhsprog + i, rhsprog + j, done, nt, a.info, a.spin_limit, s_wait);
+    int r = 0;
+    PROF(p_wait, r = dag_wait(rhsprog + i, rhsprog + j, done, nt, a.info, a.spin_limit, s_wait));
     const int nst = (min(r * DT, n) - done * DT) / DTK;  // (the last block may be short)
-    dag_accum(acc, Pcol + (size_t)done * DT, a.ldb, mv, Qcol + (size_t)done * DT, a.ldb, nv, nst,
-              lds);
+    PROF(p_acc, dag_accum(acc, Pcol + (size_t)done * DT, a.ldb, mv, Qcol + (size_t)done * DT, a.ldb,
+                          nv, nst, lds));
     done = r;
   }
 #pragma unroll
@@ -408,7 +413,7 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
       // G_ij = sum_{k >= j} B_ki^T B_kj (i <= j; B lower triangular, so row blocks k < j
       // of B_kj vanish), row blocks taken as both columns of B finalise them; written to
       // tile (i, j) and, transposed, to (j, i); no one waits for G, so nothing is published
-      if (!skip) dag_gram_task(a, (code >> 16) & 0x7fff, code & 0xffff, lds, &s_wait);
+      if (!skip) dag_gram_task(a, (code >> 16) & 0x7fff, code & 0xffff, lds, &s_wait, p_wait, p_acc);
       ++p_n;
       __syncthreads();  // every wave has read s_task before wave 0 takes the next ticket
       continue;

@@ -134,6 +134,19 @@ __device__ __forceinline__ int dag_idx(int row, int chunk) {
 // fed by LDS-DMA (global_load_lds_dwordx4, swizzle applied on the source address), DMA three
 // stages ahead, next stage's fragments read during the current stage's MFMAs.  Leaves the
 // LDS free (ends with a barrier).
+//
+// TRI (the W-products U_ij = W_i^T B, K = 128, P = W_i upper triangular: P[k + m ldp] = 0 for
+// k > m): stage s (k in [16 s, 16 s + 16)) only feeds the 16-row blocks mb >= s of the result,
+// so the MFMAs of the others are skipped.  The two wave rows take interleaved row blocks --
+// wm = 0: {0, 3, 4, 7}, wm = 1: {1, 2, 5, 6}, 18 block-stages each -- instead of halves (10 and
+// 26), so the waves stay balanced: 20 of 32 stage-slots of MFMA work per wave, with the same
+// accumulators and fragment registers.  Element (m, n) of acc[i][j][r]: m = 16 dag_mblk(wm, j)
+// + (lane & 15).
+__device__ __forceinline__ int dag_mblk(int wm, int j) {
+  return 4 * (j >> 1) + (wm ? 1 + (j & 1) : 3 * (j & 1));
+}
+
+template <bool TRI = false>
 __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __restrict__ P,
                                           size_t ldp, int mv, const double* __restrict__ Q,
                                           size_t ldq, int nv, int nst, double* lds) {
@@ -169,20 +182,25 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
       for (int i = 0; i < 4; ++i)
         F[p][i] = *reinterpret_cast<const d2*>(&qs[dag_idx(wn * 64 + i * 16 + (lane & 15), ch)]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        F[p][4 + j] = *reinterpret_cast<const d2*>(&ps[dag_idx(wm * 64 + j * 16 + (lane & 15), ch)]);
+      for (int j = 0; j < 4; ++j) {
+        const int mrow = TRI ? 16 * dag_mblk(wm, j) : wm * 64 + j * 16;
+        F[p][4 + j] = *reinterpret_cast<const d2*>(&ps[dag_idx(mrow + (lane & 15), ch)]);
+      }
     }
   };
-  auto mfma_stage = [&](const d2 (&F)[DNP][8]) {
+  auto mfma_stage = [&](const d2 (&F)[DNP][8], int s) {
+    (void)s;
 #pragma unroll
-    for (int p = 0; p < DNP; ++p)
+    for (int j = 0; j < 4; ++j) {
+      if (TRI && dag_mblk(wm, j) < s) continue;  // (wave-uniform: W_i's zeros)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int p = 0; p < DNP; ++p)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int i = 0; i < 4; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(F[p][i][h], F[p][4 + j][h], acc[i][j], 0, 0, 0);
+    }
   };
   auto step = [&](int s, d2 (&Fc)[DNP][8], d2 (&Fn)[DNP][8]) {
     // keep the previous stage's MFMAs ahead of this barrier: issued just before it, they run
@@ -195,7 +213,8 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
     __builtin_amdgcn_s_barrier();
     issue(s + DPB - 1);
     read_frags(Fn, s + 1);
-    mfma_stage(Fc);
+    mfma_stage(Fc, s);
+    if constexpr (TRI) return;  // (variable MFMA counts: the compiler's own order)
 // instruction order inside a stage (same-box C3 DAG launch, profiles/r02e_ab_dag_sched_
 // variants.txt): 0 (default) 299.8 ms, 1 300.1, 2 313.6, 3 314.1
 #ifndef DAG_SCHED
@@ -251,7 +270,7 @@ __device__ __forceinline__ void dag_accum(d4v (&acc)[4][4], const double* __rest
     step(s, F0, F1);
     step(s + 1, F1, F0);
   }
-  if (s < nst) mfma_stage(F0);
+  if (s < nst) mfma_stage(F0, s);
   dag_vmcnt<0>();
   __syncthreads();
 }
@@ -498,7 +517,12 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = d4v{0.0, 0.0, 0.0, 0.0};
-        PROF(p_tri, dag_accum(acc, a.winv + (size_t)i * DT * DT, DT, mv, T, ldt, nv, mv / DTK, lds));
+        // (full tiles: the triangular form; the last tile row, mv < 128, the plain one)
+        const bool tri = mv == DT;
+        if (tri)
+          PROF(p_tri, dag_accum<true>(acc, a.winv + (size_t)i * DT * DT, DT, mv, T, ldt, nv, DT / DTK, lds));
+        else
+          PROF(p_tri, dag_accum(acc, a.winv + (size_t)i * DT * DT, DT, mv, T, ldt, nv, mv / DTK, lds));
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -506,7 +530,7 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
             const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
-              const int mm = wm * 64 + jj * 16 + (lane & 15);
+              const int mm = (tri ? 16 * dag_mblk(wm, jj) : wm * 64 + jj * 16) + (lane & 15);
               if (mm < mv && nn < nv) st_res<true>(&T[(size_t)mm + (size_t)nn * ldt], acc[ii][jj][r]);
             }
           }

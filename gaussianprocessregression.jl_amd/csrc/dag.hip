@@ -321,11 +321,17 @@ __device__ __forceinline__ void dag_publish(int* prog, int v) {
 // The F task's factorisation, out of line: inlined, its readlane-heavy elimination (SGPR
 // spills into VGPR lanes) shares the allocation with the GEMM pipeline's live state and
 // spilled to scratch; as a call it is allocated on its own.
-__device__ __attribute__((noinline)) int dag_factor(double* S, double* T, size_t lda, int mv,
-                                                     int kglob, double* winv) {
+// (U_ii itself is NOT stored here: no task of the launch reads a diagonal tile -- every
+// accumulation takes U_ki with k < i, the off-diagonal and right-hand-side tiles take W_i -- so
+// the task publishes once W_i is out and stores U_ii afterwards, off the chain: dag_store_u)
+__device__ __attribute__((noinline)) int dag_factor(double* S, int mv, int kglob, double* winv) {
   double(*Xd)[D2_PB] = reinterpret_cast<double(*)[D2_PB]>(S + D2_PK);
   int* fail = reinterpret_cast<int*>(S + D2_PK + 4 * D2_PB);
-  return diag2_core<true>(S, Xd, fail, T, lda, mv, kglob, winv);
+  return diag2_core<true>(S, Xd, fail, nullptr, 0, mv, kglob, winv);
+}
+
+__device__ __attribute__((noinline)) void dag_store_u(const double* S, double* T, size_t lda, int mv) {
+  diag2_store_u(S, T, lda, mv);
 }
 
 // A gram task: K^{-1} = Z^T Z tile (i, j), i <= j.  Inlined into the GRAM instance of the
@@ -401,6 +407,7 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
   int& s_task = reinterpret_cast<int*>(lds + DINT)[0];
   int& s_skip = reinterpret_cast<int*>(lds + DINT)[1];
   int& s_wait = reinterpret_cast<int*>(lds + DINT)[2];
+  int s_fok = 0;  // this diagonal task factored its tile (uniform)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w & 1, wn = w >> 1;
@@ -491,8 +498,9 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
         __syncthreads();
         DTRACE(1, 3);
         int f = 0;
-        PROF(p_fac, f = dag_factor(S, T, a.lda, mv, a.kglob + i * DT, a.winv + (size_t)i * DT * DT));
+        PROF(p_fac, f = dag_factor(S, mv, a.kglob + i * DT, a.winv + (size_t)i * DT * DT));
         if (f && w == 0) atomicCAS(a.info, 0, f);
+        s_fok = f == 0;
         DTRACE(1, 4);
       } else {
         // B_ij = -acc into the tile (own tile: only this workgroup reads it back), then
@@ -539,6 +547,8 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
     DTRACE(1, 5);
     dag_publish(pj, i + 1);
     DTRACE(1, 6);
+    // U_ii after the publish (read by later launches only; the LDS still holds it)
+    if (diag && !skip && __builtin_amdgcn_readfirstlane(s_fok)) dag_store_u(lds, T, a.lda, mv);
     ++p_n;
   }
   DTRACE(1, 7);

@@ -302,12 +302,16 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
     if (sb == 0) STAMP(6);
   }
   STAMP(2);
-  // U back to global (fire-and-forget; nothing below waits for these stores)
+  // U back to global (fire-and-forget; nothing below waits for these stores).  Ab = nullptr:
+  // the caller stores U later (diag2_store_u) -- the tile-DAG, where no task of the launch
+  // reads a diagonal tile, publishes W first
+  if (Ab) {
 #pragma unroll
-  for (int e = 0; e < PER; ++e) {
-    const int idx = tid + e * DIAG_THREADS;
-    const int r = idx % NB, c = idx / NB;
-    if (r < kb && c < kb && r <= c) st_res<SC1>(&Ab[(size_t)r + (size_t)c * lda], S[pk(r, c)]);
+    for (int e = 0; e < PER; ++e) {
+      const int idx = tid + e * DIAG_THREADS;
+      const int r = idx % NB, c = idx / NB;
+      if (r < kb && c < kb && r <= c) st_res<SC1>(&Ab[(size_t)r + (size_t)c * lda], S[pk(r, c)]);
+    }
   }
   // W = U^-1, one wave per column half (MFMA work 144 / 144 / 112 / 112)
   if (wv == 0) {
@@ -322,6 +326,18 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
   }
   STAMP(4);
   return 0;
+}
+
+// U (kb x kb upper, from S) to Ab with plain stores
+__device__ __forceinline__ void diag2_store_u(const double* __restrict__ S, double* __restrict__ Ab,
+                                              size_t lda, int kb) {
+  constexpr int NB = D2_NB, PER = NB * NB / DIAG_THREADS;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int idx = threadIdx.x + e * DIAG_THREADS;
+    const int r = idx % NB, c = idx / NB;
+    if (r < kb && c < kb && r <= c) Ab[(size_t)r + (size_t)c * lda] = S[pk(r, c)];
+  }
 }
 
 }  // namespace

@@ -269,16 +269,19 @@ struct StreamOut {
 int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
   gpr_mgpu* h = so->h;
   auto& R = h->rccl;
+  // every chunk's broadcast is issued even after a failed launch (the receivers are already
+  // waiting in the matching calls; the host reports the error afterwards) -- only a failing
+  // RCCL call ends the loop
   int rc = 0;
   if (hipStreamWaitEvent(h->sp, dep, 0) != hipSuccess) rc = GPR_E_HIP;
-  for (size_t c = 0; rc == 0 && c + 1 < so->rows.size(); ++c) {
+  for (size_t c = 0; c + 1 < so->rows.size(); ++c) {
     const int r0 = so->rows[c], r1 = so->rows[c + 1];
     double* slice = so->pk + rows_base(r0, so->n);
     const size_t len = chunk_len(r0, r1, so->n);
     if (colprog) rows_gate_kernel<<<1, 256, 0, h->sp>>>(colprog, nt, r0, r1, so->limit, h->derr);
     launch_rows_pack(h->sp, so->U, so->n, so->n, r0, r1, so->pk, true);
-    if (hipGetLastError() != hipSuccess ||
-        R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess) {
+    if (hipGetLastError() != hipSuccess) rc = GPR_E_HIP;
+    if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess) {
       rc = GPR_E_HIP;
       break;
     }

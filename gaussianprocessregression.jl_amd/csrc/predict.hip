@@ -805,10 +805,14 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
                               ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise, sizeof(double) * ny, hipMemcpyHostToDevice,
                               ctx->stream));
-  // LAPACK.syevr!(ws, 'V', 'A', 'U', kxx, ...) -> eigenvalues ascending, eigenvectors in K
+  // LAPACK.syevr!(ws, 'V', 'A', 'U', kxx, ...) -> eigenvalues ascending, eigenvectors in K.
+  // A call the library refuses (e.g. a rocSOLVER without code for this device) leaves K
+  // untouched: the caller then factors per column instead
   if (g_rs.dsyevd(hb, rocblas_evect_original, rocblas_fill_upper, n, K, n, lam, E, dinfo) !=
-      rocblas_status_success)
-    return set_err(ctx, GPR_E_HIP, "rocsolver_dsyevd failed");
+      rocblas_status_success) {
+    (void)hipGetLastError();
+    return 1;
+  }
   int hinfo = 0;
   HIP_TRY(ctx, hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   // T = P^T B
@@ -856,7 +860,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   const char* qe = getenv("GPR_QUAD_EIGEN");
   if (!qe || atoi(qe) != 0) {
     const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var);
-    if (rc != 1) return rc;  // (1: rocSOLVER unavailable)
+    if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
   }
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);
   if (n > 8192) nsub = 1;

@@ -94,8 +94,10 @@ struct gpr_ctx {
   // counters are reset (null if it could not be made): work ordered behind that event runs
   // BESIDE the launch (mgpu.hip streams finished tile rows of U out to the other GPUs); cleared
   // before the call
-  void (*dag_hook)(void* user, const double* dA, int n, int lda, const int* colprog, int nt,
-                   hipEvent_t counters_reset) = nullptr;
+  // (colprog: the progress counters; ustored[i] = 1 once the diagonal tile U_ii is stored --
+  // the launch raises colprog before that store)
+  void (*dag_hook)(void* user, const double* dA, int n, int lda, const int* colprog,
+                   const int* ustored, int nt, hipEvent_t counters_reset) = nullptr;
   void* dag_hook_user = nullptr;
   int dag_reserve_cu = 0;  // CUs the persistent grid leaves free for such concurrent work
   bool rhs_solved = false; // the last potrf_core solved its RhsSpec (not dropped by its block sizes)

@@ -103,6 +103,8 @@ struct DagArgs {
   int kglob;     // global index of row 0 (reported pivot orders)
   int* info;
   int* sync;     // [0] ticket, [2 + j] colprog[j], [2 + nt + c] rhsprog[c]
+  int* ustored;  // optional (a launch hook reads U while the launch runs): ustored[i] = 1 once
+                 // U_ii's (post-publish) store has drained -- colprog alone does not cover it
   const unsigned* tasks;
   int ntasks;
   int lower;     // B is lower triangular (the identity's solve Z = U^{-T}): tile (i, c) exists
@@ -330,8 +332,14 @@ __device__ __attribute__((noinline)) int dag_factor(double* S, int mv, int kglob
   return diag2_core<true>(S, Xd, fail, nullptr, 0, mv, kglob, winv);
 }
 
-__device__ __attribute__((noinline)) void dag_store_u(const double* S, double* T, size_t lda, int mv) {
-  diag2_store_u(S, T, lda, mv);
+// (sc1: a launch hook's kernel reads U_ii on another stream while the launch runs -- a plain
+// store would sit in this XCD's L2 until the launch ends)
+__device__ __attribute__((noinline)) void dag_store_u(const double* S, double* T, size_t lda, int mv,
+                                                      bool sc1) {
+  if (sc1)
+    diag2_store_u<true>(S, T, lda, mv);
+  else
+    diag2_store_u<false>(S, T, lda, mv);
 }
 
 // A gram task: K^{-1} = Z^T Z tile (i, j), i <= j.  Inlined into the GRAM instance of the
@@ -548,7 +556,12 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
     dag_publish(pj, i + 1);
     DTRACE(1, 6);
     // U_ii after the publish (read by later launches only; the LDS still holds it)
-    if (diag && !skip && __builtin_amdgcn_readfirstlane(s_fok)) dag_store_u(lds, T, a.lda, mv);
+    if (diag && !skip && __builtin_amdgcn_readfirstlane(s_fok))
+      dag_store_u(lds, T, a.lda, mv, a.ustored != nullptr);
+    // ... and by a launch hook's readers (the streamed broadcast's row gates): they wait for
+    // ustored[i] too, raised once the (then write-through) store drained -- also after a
+    // failure, so no gate waits out its limit; the host reports the error
+    if (diag && a.ustored) dag_publish(a.ustored + i, 1);
     ++p_n;
   }
   DTRACE(1, 7);
@@ -719,7 +732,8 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_flags = flags;
     ctx->dag_lag_built = (ctx->dag_zlag * 1024 + ctx->dag_rlag) * 2 + ctx->dag_fearly;
   }
-  const size_t nsync = 2 + (size_t)nt + ntr;
+  // [2 + nt + ntr + i]: ustored[i] (hook launches; zeroed with the rest)
+  const size_t nsync = 2 + (size_t)nt + ntr + nt;
   if (ctx->dag_sync_cap < nsync) {
     if (ctx->dag_sync) {
       HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (every DAG launch joins it)
@@ -767,6 +781,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   // hook itself only after the launch is enqueued -- work it orders behind the event can then
   // never sit ahead of the launch in a hardware queue that two streams share
   auto hook = (ctx->dag_hook && !solve && !lower && kglob == 0) ? ctx->dag_hook : nullptr;
+  a.ustored = hook ? ctx->dag_sync + 2 + nt + ntr : nullptr;
   hipEvent_t hook_ev = nullptr;
   if (hook) {
     ctx->dag_hook = nullptr;
@@ -793,7 +808,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     LAUNCH_CHECK(ctx);
   }
   if (hook) {
-    hook(ctx->dag_hook_user, dA, n, lda, ctx->dag_sync + 2, nt, hook_ev);
+    hook(ctx->dag_hook_user, dA, n, lda, ctx->dag_sync + 2, a.ustored, nt, hook_ev);
     if (hook_ev) hipEventDestroy(hook_ev);
   }
   return 0;

@@ -328,7 +328,9 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
   return 0;
 }
 
-// U (kb x kb upper, from S) to Ab with plain stores
+// U (kb x kb upper, from S) to Ab: plain stores (read by later launches only), or sc1
+// (write-through: read by another stream's kernel while this launch runs)
+template <bool SC1>
 __device__ __forceinline__ void diag2_store_u(const double* __restrict__ S, double* __restrict__ Ab,
                                               size_t lda, int kb) {
   constexpr int NB = D2_NB, PER = NB * NB / DIAG_THREADS;
@@ -336,7 +338,7 @@ __device__ __forceinline__ void diag2_store_u(const double* __restrict__ S, doub
   for (int e = 0; e < PER; ++e) {
     const int idx = threadIdx.x + e * DIAG_THREADS;
     const int r = idx % NB, c = idx / NB;
-    if (r < kb && c < kb && r <= c) Ab[(size_t)r + (size_t)c * lda] = S[pk(r, c)];
+    if (r < kb && c < kb && r <= c) st_res<SC1>(&Ab[(size_t)r + (size_t)c * lda], S[pk(r, c)]);
   }
 }
 

@@ -150,9 +150,12 @@ __global__ __launch_bounds__(256) void rows_pack_kernel(double* __restrict__ U, 
 
 // Waits until tile rows [r0, r1) of U are final in a running tile-DAG launch: colprog[j] (final
 // tiles at the top of tile column j, raised with sc1 stores after the tiles' sc1 stores drained)
-// >= min(r1, j + 1) for every j >= r0.  Bounded like the DAG's own waits: after `limit` polls
-// it flags *err and returns (the chunk then carries garbage and the host reports the error).
-__global__ __launch_bounds__(256) void rows_gate_kernel(const int* __restrict__ colprog, int nt,
+// >= min(r1, j + 1) for every j >= r0, and ustored[j] for the diagonal tiles j in [r0, r1) (a
+// diagonal task publishes colprog once W_j is out and stores U_jj after that).  Bounded like
+// the DAG's own waits: after `limit` polls it flags *err and returns (the chunk then carries
+// garbage and the host reports the error).
+__global__ __launch_bounds__(256) void rows_gate_kernel(const int* __restrict__ colprog,
+                                                        const int* __restrict__ ustored, int nt,
                                                         int r0, int r1, long long limit,
                                                         int* __restrict__ err) {
   long long spins = 0;
@@ -160,7 +163,9 @@ __global__ __launch_bounds__(256) void rows_gate_kernel(const int* __restrict__ 
     int ok = limit > 0;  // (limit 0: give up at once)
     for (int j = r0 + (int)threadIdx.x; j < nt; j += 256)
       ok &= __hip_atomic_load(colprog + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-            min(r1, j + 1);
+                min(r1, j + 1) &&
+            (j >= r1 ||
+             __hip_atomic_load(ustored + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0);
     if (__syncthreads_and(ok)) break;
     if (++spins > limit) {  // (spins is the same in every thread: a uniform exit)
       if (threadIdx.x == 0) atomicExch(err, 1);
@@ -266,7 +271,7 @@ struct StreamOut {
 };
 
 // (dep: the event the chunks wait for -- the counters' reset, or the end of the fit)
-int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
+int enqueue_chunks(StreamOut* so, const int* colprog, const int* ustored, int nt, hipEvent_t dep) {
   gpr_mgpu* h = so->h;
   auto& R = h->rccl;
   // every chunk's broadcast is issued even after a failed launch (the receivers are already
@@ -278,7 +283,8 @@ int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
     const int r0 = so->rows[c], r1 = so->rows[c + 1];
     double* slice = so->pk + rows_base(r0, so->n);
     const size_t len = chunk_len(r0, r1, so->n);
-    if (colprog) rows_gate_kernel<<<1, 256, 0, h->sp>>>(colprog, nt, r0, r1, so->limit, h->derr);
+    if (colprog)
+      rows_gate_kernel<<<1, 256, 0, h->sp>>>(colprog, ustored, nt, r0, r1, so->limit, h->derr);
     launch_rows_pack(h->sp, so->U, so->n, so->n, r0, r1, so->pk, true);
     if (hipGetLastError() != hipSuccess) rc = GPR_E_HIP;
     if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess) {
@@ -293,11 +299,11 @@ int enqueue_chunks(StreamOut* so, const int* colprog, int nt, hipEvent_t dep) {
 // The tile-DAG launch's hook on device 0 (called right after the launch is enqueued): the
 // gates, packs and broadcasts go on sp behind the counters' reset, i.e. beside the launch.
 // A padded copy (other shapes) or a missing event: nothing here, the chunks follow the fit.
-void stream_out_hook(void* user, const double* dA, int n, int lda, const int* colprog, int nt,
-                     hipEvent_t counters_reset) {
+void stream_out_hook(void* user, const double* dA, int n, int lda, const int* colprog,
+                     const int* ustored, int nt, hipEvent_t counters_reset) {
   auto* so = static_cast<StreamOut*>(user);
-  if (!counters_reset || dA != so->U || n != so->n || lda != so->n) return;
-  so->rc = enqueue_chunks(so, colprog, nt, counters_reset);
+  if (!counters_reset || !ustored || dA != so->U || n != so->n || lda != so->n) return;
+  so->rc = enqueue_chunks(so, colprog, ustored, nt, counters_reset);
   so->fired = true;
 }
 
@@ -569,7 +575,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     if (hipEventCreateWithFlags(&fit_done, hipEventDisableTiming) != hipSuccess ||
         hipEventRecord(fit_done, s) != hipSuccess)
       prc = GPR_E_HIP;
-    if (prc == 0 && !so.fired) prc = enqueue_chunks(&so, nullptr, 0, fit_done);
+    if (prc == 0 && !so.fired) prc = enqueue_chunks(&so, nullptr, nullptr, 0, fit_done);
     if (prc == 0 && hipStreamWaitEvent(h->sp, fit_done, 0) != hipSuccess) prc = GPR_E_HIP;
     if (prc == 0 && R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess)
       prc = GPR_E_HIP;

@@ -422,6 +422,10 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
   int* colprog = a.sync + 2;
   int* rhsprog = colprog + a.nt;
   unsigned long long p_wait = 0, p_acc = 0, p_fac = 0, p_tri = 0, p_all = 0, p_n = 0;
+#ifdef DAG_PROF_PUB
+  unsigned long long p_pub = 0, p_tri_unused = 0;
+#define p_tri p_tri_unused
+#endif
   (void)p_wait; (void)p_acc; (void)p_fac; (void)p_tri; (void)p_all; (void)p_n;
 #ifdef DAG_TRACE
   const unsigned long long p_start = __builtin_amdgcn_s_memrealtime();
@@ -553,7 +557,12 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
       }
     }
     DTRACE(1, 5);
+#ifdef DAG_PROF_PUB
+    // (probe build: the "trsm" slot times the diagonal tasks' publish -- W_i's store drain)
+    if (diag) PROF(p_pub, dag_publish(pj, i + 1)); else dag_publish(pj, i + 1);
+#else
     dag_publish(pj, i + 1);
+#endif
     DTRACE(1, 6);
     // U_ii after the publish (read by later launches only; the LDS still holds it)
     if (diag && !skip && __builtin_amdgcn_readfirstlane(s_fok))
@@ -570,7 +579,13 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
   DTRACE(2, (int)p_wait);
   DTRACE(3, (int)p_acc);
   DTRACE(4, (int)p_fac);
+#ifdef DAG_PROF_PUB
+#undef p_tri
+  DTRACE(5, (int)p_pub);
+  (void)p_tri_unused;
+#else
   DTRACE(5, (int)p_tri);
+#endif
   DTRACE(6, (int)p_all);
   DTRACE(7, (int)p_n);
 #endif

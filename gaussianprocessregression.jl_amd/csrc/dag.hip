@@ -35,6 +35,32 @@
 #include <algorithm>
 #include <cstdint>
 
+#include "common.hpp"
+
+#ifdef DAG_TRACE
+// diagnostic build: the diagonal factor's phases (band sb elimination: 2 sb, its trailing
+// update: 2 sb + 1, the inverse: 7; realtime ticks summed over the launch's diagonal tasks)
+__device__ unsigned long long g_diag_ph[16];
+#define DSTAMP_INIT() unsigned long long _dst_t = __builtin_amdgcn_s_memrealtime()
+#define DSTAMP(i)                                                   \
+  do {                                                              \
+    __syncthreads();                                                \
+    if (threadIdx.x == 0) {                                         \
+      const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+      atomicAdd(&g_diag_ph[i], _t - _dst_t);                        \
+      if ((i) == 7) atomicAdd(&g_diag_ph[8], 1ull);                 \
+      _dst_t = _t;                                                  \
+    }                                                               \
+  } while (0)
+extern "C" void gpr_debug_diag_phases(unsigned long long* out, int reset) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_ph), sizeof(unsigned long long) * 16);
+  if (reset) {
+    unsigned long long z[16] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_diag_ph), z, sizeof z);
+  }
+}
+#endif
+
 #include "diag_block.hpp"
 
 #ifdef DAG_TRACE
@@ -327,19 +353,21 @@ __device__ __forceinline__ void dag_publish(int* prog, int v) {
 // accumulation takes U_ki with k < i, the off-diagonal and right-hand-side tiles take W_i -- so
 // the task publishes once W_i is out and stores U_ii afterwards, off the chain: dag_store_u)
 __device__ __attribute__((noinline)) int dag_factor(double* S, int mv, int kglob, double* winv) {
-  double(*Xd)[D2_PB] = reinterpret_cast<double(*)[D2_PB]>(S + D2_PK);
-  int* fail = reinterpret_cast<int*>(S + D2_PK + 4 * D2_PB);
-  return diag2_core<true>(S, Xd, fail, nullptr, 0, mv, kglob, winv);
+  lds_d* L = (lds_d*)S;  // (one conversion; see diag_block.hpp)
+  lds_d(*Xd)[D2_PB] = reinterpret_cast<lds_d(*)[D2_PB]>(L + D2_PK);
+  lds_i* fail = reinterpret_cast<lds_i*>(L + D2_PK + 4 * D2_PB);
+  return diag2_core<true>(L, Xd, fail, nullptr, 0, mv, kglob, winv);
 }
 
 // (sc1: a launch hook's kernel reads U_ii on another stream while the launch runs -- a plain
 // store would sit in this XCD's L2 until the launch ends)
 __device__ __attribute__((noinline)) void dag_store_u(const double* S, double* T, size_t lda, int mv,
                                                       bool sc1) {
+  const lds_d* L = (const lds_d*)S;
   if (sc1)
-    diag2_store_u<true>(S, T, lda, mv);
+    diag2_store_u<true>(L, T, lda, mv);
   else
-    diag2_store_u<false>(S, T, lda, mv);
+    diag2_store_u<false>(L, T, lda, mv);
 }
 
 // A gram task: K^{-1} = Z^T Z tile (i, j), i <= j.  Inlined into the GRAM instance of the

@@ -10,6 +10,15 @@
   do {           \
   } while (0)
 #endif
+// phase timers of the tile-DAG's diagonal factor (dag.hip's DAG_TRACE build defines them)
+#ifndef DSTAMP
+#define DSTAMP_INIT() \
+  do {                \
+  } while (0)
+#define DSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
 
 namespace {
 
@@ -17,6 +26,12 @@ constexpr int DIAG_THREADS = 256;
 
 typedef double d4v __attribute__((ext_vector_type(4)));
 typedef double d2v __attribute__((ext_vector_type(2)));
+// LDS-typed pointers: the tile-DAG calls the factor out of line, and through a generic pointer
+// every LDS access became a flat-to-local conversion with its own null check and the trailing
+// update's loads were issued one at a time
+typedef __attribute__((address_space(3))) double lds_d;
+typedef __attribute__((address_space(3))) int lds_i;
+typedef __attribute__((address_space(3))) d2v lds_d2v;
 
 __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -38,12 +53,17 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // Global store of a result another workgroup of the SAME launch may read after a flag
 // (SC1: sc1 = write-through, the line leaves this XCD's L2 -- the MI355X guide's sc1
 // hand-off), or a plain store (results read only by later launches).
+// (through a global-typed pointer: out of line -- the tile-DAG's factor -- a generic pointer
+// made these flat stores, which also count in lgkmcnt, so every later LDS wait of the inverse
+// waited for the write-through stores too)
+typedef __attribute__((address_space(1))) double glb_d;
 template <bool SC1>
 __device__ __forceinline__ void st_res(double* p, double v) {
+  glb_d* g = (glb_d*)p;
   if constexpr (SC1)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else
-    *p = v;
+    *g = v;
 }
 
 // ---- diag kernel v2 (NB = 128, factor mode): no per-pivot workgroup barriers ------------
@@ -77,8 +97,8 @@ constexpr int D2_LDS_DOUBLES = D2_PIV + 4 * 64;
 
 // column half (J, jh) of W = U^-1 (see above); S = U packed upper (128), Xd = packed diag inverses
 template <int J, bool SC1>
-__device__ __forceinline__ void d2_inv_colhalf(int jh, const double* __restrict__ S,
-                                               const double (*__restrict__ Xd)[D2_PB],
+__device__ __forceinline__ void d2_inv_colhalf(int jh, const lds_d* __restrict__ S,
+                                               const lds_d (*__restrict__ Xd)[D2_PB],
                                                double* __restrict__ winv, int kb, int lane) {
   d4v X[J + 1][2];
   const int col = 16 * jh + (lane & 15);  // column within block J
@@ -135,7 +155,7 @@ __device__ __forceinline__ void d2_inv_colhalf(int jh, const double* __restrict_
 // Batched loads, 4 x 16 in flight: thread t owns row r = t % 128 of columns c0 + 2e.  Clamped
 // addresses + select: every load is issued unconditionally (a branch around a load makes the
 // compiler drain vmcnt on the other path, serialising the batch).
-__device__ __forceinline__ void diag2_load(double* __restrict__ S, const double* __restrict__ Ab,
+__device__ __forceinline__ void diag2_load(lds_d* __restrict__ S, const double* __restrict__ Ab,
                                            size_t lda, int kb) {
   constexpr int PER = D2_NB * D2_NB / DIAG_THREADS;
   const int tid = threadIdx.x;
@@ -160,14 +180,15 @@ __device__ __forceinline__ void diag2_load(double* __restrict__ S, const double*
 // the first non-positive pivot -- then nothing is written.  Uniform across the workgroup.
 // Xd: 4 x D2_PB doubles of LDS; fail: one int of LDS.
 template <bool SC1>
-__device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__restrict__ Xd)[D2_PB],
-                                          int* fail, double* __restrict__ Ab, size_t lda, int kb,
+__device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restrict__ Xd)[D2_PB],
+                                          lds_i* fail, double* __restrict__ Ab, size_t lda, int kb,
                                           int kglob, double* __restrict__ winv) {
   constexpr int NB = D2_NB, PER = NB * NB / DIAG_THREADS;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (wv == 0) *fail = 0;  // (wave-uniform branch)
   __syncthreads();
+  DSTAMP_INIT();
 #pragma unroll 1
   for (int sb = 0; sb < 4; ++sb) {
     const int K0 = 32 * sb, W = NB - K0;
@@ -196,7 +217,7 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
       // needs as 16-B broadcasts -- one ds_write + (31 - j) / 2 ds_reads per step instead of
       // two v_readlane per entry.  A wave's LDS operations complete in order, so the next
       // step's write cannot overtake this step's reads; no other wave touches the buffer.
-      double* pivb = S + D2_PIV + 64 * wv;
+      lds_d* pivb = S + D2_PIV + 64 * wv;
 #endif
 #pragma unroll
       for (int j = 0; j < 32; ++j) {
@@ -217,7 +238,7 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
           d2v r2[8];
 #pragma unroll
           for (int t = 0; t < 8; ++t)
-            if (g0 + 2 * t < 32) r2[t] = *reinterpret_cast<const d2v*>(pivb + g0 + 2 * t);
+            if (g0 + 2 * t < 32) r2[t] = *reinterpret_cast<const lds_d2v*>(pivb + g0 + 2 * t);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int t = 0; t < 8; ++t) {
@@ -267,39 +288,74 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
     }
     __syncthreads();
     if (sb == 0) STAMP(5);
+    DSTAMP(2 * sb);
     const int f = __builtin_amdgcn_readfirstlane(*fail);  // uniform branch around barriers
     if (f) return f;
     const int R = W - 32;
     if (R <= 0) break;
-    // F3: U(r, c) -= sum_p U(K0+p, r) U(K0+p, c) for K0+32 <= r <= c < NB, on MFMA
+    // F3: U(r, c) -= sum_p U(K0+p, r) U(K0+p, c) for K0+32 <= r <= c < NB, on MFMA.  A wave
+    // takes two 16 x 16 tiles per pass (t and t + 4): every operand and the old values are
+    // loaded first (a sched barrier keeps the compiler from sinking each load next to its
+    // MFMA, which serialised load -> wait -> MFMA), then the two tiles' MFMA chains interleave
     {
       const int nt = R / 16, B0 = K0 + 32;
       const int ntile = nt * (nt + 1) / 2;
-      for (int t = wv; t < ntile; t += DIAG_THREADS / 64) {
+      auto tile_of = [&](int t, int& r0, int& q0) {
         int tj = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
         while ((tj + 1) * (tj + 2) / 2 <= t) ++tj;
         while (tj * (tj + 1) / 2 > t) --tj;
-        const int ti = t - tj * (tj + 1) / 2;
-        const int r0 = B0 + 16 * ti, q0 = B0 + 16 * tj;
-        double av[8], bv[8];
+        r0 = B0 + 16 * (t - tj * (tj + 1) / 2);
+        q0 = B0 + 16 * tj;
+      };
+      for (int t = wv; t < ntile; t += 2 * (DIAG_THREADS / 64)) {
+        const int t1 = t + DIAG_THREADS / 64;
+        const bool two = t1 < ntile;  // (wave-uniform)
+        int r0, q0, r1, q1;
+        tile_of(t, r0, q0);
+        tile_of(two ? t1 : t, r1, q1);
+        double av0[8], bv0[8], av1[8], bv1[8], o0[4], o1[4];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
           const int p = K0 + 4 * kk + (lane >> 4);
-          av[kk] = S[pk(p, r0 + (lane & 15))];
-          bv[kk] = S[pk(p, q0 + (lane & 15))];
+          av0[kk] = S[pk(p, r0 + (lane & 15))];
+          bv0[kk] = S[pk(p, q0 + (lane & 15))];
+          av1[kk] = S[pk(p, r1 + (lane & 15))];
+          bv1[kk] = S[pk(p, q1 + (lane & 15))];
         }
-        d4v acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], bv[kk], acc, 0, 0, 0);
+        for (int qq = 0; qq < 4; ++qq) {
+          const int c0 = q0 + (lane & 15), rr0 = min(r0 + (lane >> 4) + 4 * qq, c0);
+          const int c1 = q1 + (lane & 15), rr1 = min(r1 + (lane >> 4) + 4 * qq, c1);
+          o0[qq] = S[pk(rr0, c0)];
+          o1[qq] = S[pk(rr1, c1)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {  // (the barriers keep the two chains interleaved)
+          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[kk], bv0[kk], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1[kk], bv1[kk], acc1, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // branch-free stores: entries below the diagonal (and the second tile when !two) go to
+        // this wave's pivot-row buffer, unused here -- with exec-masked stores the compiler
+        // sank the second chain's MFMAs behind the first tile's stores
+        lds_d* dump = S + D2_PIV + 64 * wv + lane;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const int r = r0 + (lane >> 4) + 4 * qq, c = q0 + (lane & 15);
-          if (r <= c) S[pk(r, c)] -= acc[qq];
+          *(r <= c ? S + pk(r, c) : dump) = o0[qq] - acc0[qq];
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int r = r1 + (lane >> 4) + 4 * qq, c = q1 + (lane & 15);
+          *(two && r <= c ? S + pk(r, c) : dump) = o1[qq] - acc1[qq];
         }
       }
     }
     __syncthreads();
     if (sb == 0) STAMP(6);
+    DSTAMP(2 * sb + 1);
   }
   STAMP(2);
   // U back to global (fire-and-forget; nothing below waits for these stores).  Ab = nullptr:
@@ -325,13 +381,14 @@ __device__ __forceinline__ int diag2_core(double* __restrict__ S, double (*__res
     d2_inv_colhalf<0, SC1>(jh, S, Xd, winv, kb, lane);
   }
   STAMP(4);
+  DSTAMP(7);
   return 0;
 }
 
 // U (kb x kb upper, from S) to Ab: plain stores (read by later launches only), or sc1
 // (write-through: read by another stream's kernel while this launch runs)
 template <bool SC1>
-__device__ __forceinline__ void diag2_store_u(const double* __restrict__ S, double* __restrict__ Ab,
+__device__ __forceinline__ void diag2_store_u(const lds_d* __restrict__ S, double* __restrict__ Ab,
                                               size_t lda, int kb) {
   constexpr int NB = D2_NB, PER = NB * NB / DIAG_THREADS;
 #pragma unroll

@@ -373,9 +373,9 @@ __global__ __launch_bounds__(DIAG_THREADS, 2) void diag2_kernel(double* __restri
                                                                 int* __restrict__ info,
                                                                 double* __restrict__ winv) {
   extern __shared__ double dsm[];
-  double* S = dsm;                                               // U, packed upper (66 KB)
-  double(*Xd)[D2_PB] = reinterpret_cast<double(*)[D2_PB]>(dsm + D2_PK);  // U^-1 diag blocks
-  int* fail = reinterpret_cast<int*>(dsm + D2_PK + 4 * D2_PB);
+  lds_d* S = (lds_d*)dsm;                                        // U, packed upper (66 KB)
+  lds_d(*Xd)[D2_PB] = reinterpret_cast<lds_d(*)[D2_PB]>(S + D2_PK);  // U^-1 diag blocks
+  lds_i* fail = reinterpret_cast<lds_i*>(S + D2_PK + 4 * D2_PB);
   if (*info != 0) return;
   // this latency-bound chain shares CUs with the MFMA-saturating trailing update: take
   // issue priority over the co-resident GEMM waves

@@ -52,6 +52,13 @@ __device__ unsigned long long g_diag_ph[16];
       _dst_t = _t;                                                  \
     }                                                               \
   } while (0)
+// wave 0 only, no barrier (inside the band elimination): 9 loads, 10 elimination, 11 stores
+#define DSTAMPW(i)                                                  \
+  do {                                                              \
+    const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0) atomicAdd(&g_diag_ph[i], _t - _dst_t);    \
+    _dst_t = _t;                                                    \
+  } while (0)
 extern "C" void gpr_debug_diag_phases(unsigned long long* out, int reset) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_ph), sizeof(unsigned long long) * 16);
   if (reset) {

@@ -18,6 +18,9 @@
 #define DSTAMP(i) \
   do {            \
   } while (0)
+#define DSTAMPW(i) \
+  do {             \
+  } while (0)
 #endif
 
 namespace {
@@ -210,6 +213,7 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int r = 0; r < 32; ++r) x[r] = il ? (r == q ? 1.0 : 0.0) : ((dl && r > lane) ? 0.0 : x[r]);
+      DSTAMPW(9);
       int bad = 0;
 #ifndef D2_READLANE_ROWS
       // the pivot row through this wave's own LDS buffer: every lane writes its x[j] (lanes
@@ -270,6 +274,7 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
         }
 #endif
       }
+      DSTAMPW(10);
       if (dl) {
         if (wv == 0) {
 #pragma unroll
@@ -285,6 +290,7 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
         for (int r = 0; r < 32; ++r) S[pk(K0 + r, K0 + c)] = x[r];
       }
       if (wv == 0 && lane == 0 && bad) *fail = kglob + K0 + bad;
+      DSTAMPW(11);
     }
     __syncthreads();
     if (sb == 0) STAMP(5);

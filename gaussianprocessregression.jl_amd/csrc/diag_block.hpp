@@ -136,9 +136,12 @@ __device__ __forceinline__ void d2_inv_colhalf(int jh, const lds_d* __restrict__
       for (int st = 0; st < 8; ++st) {
         const int m = 4 * st + (lane >> 4);
         const double xv = Xd[I][pk(min(i, m), m)];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(i <= m ? xv : 0.0, T[st >> 2][st & 3], acc, 0, 0, 0);
+        // (-Xd_I as the A operand: the result is X_IJ itself, which feeds the next level's
+        // MFMAs straight from the accumulators -- negating acc moved it through VGPRs on the
+        // level-to-level chain)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(i <= m ? -xv : 0.0, T[st >> 2][st & 3], acc, 0, 0, 0);
       }
-      X[I][ih] = -acc;
+      X[I][ih] = acc;
     }
   }
   const int gc = 32 * J + col;

@@ -183,7 +183,8 @@ __device__ __forceinline__ void diag2_load(lds_d* __restrict__ S, const double* 
 // Factor the block in S (packed upper, loaded, identity padding beyond kb; the caller has
 // synchronised after filling it), write U to Ab (upper part only) and W = U^{-1} to winv
 // (128 x 128, zero outside kb x kb).  Returns 0, or the global order (kglob + row + 1) of
-// the first non-positive pivot -- then nothing is written.  Uniform across the workgroup.
+// the first non-positive pivot -- then U is not written (W's workspace slot may hold its first
+// column blocks).  Uniform across the workgroup.
 // Xd: 4 x D2_PB doubles of LDS; fail: one int of LDS.
 template <bool SC1>
 __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restrict__ Xd)[D2_PB],
@@ -294,6 +295,20 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
       }
       if (wv == 0 && lane == 0 && bad) *fail = kglob + K0 + bad;
       DSTAMPW(11);
+    } else if (sb >= 2 && wv >= 2) {
+      // W's early column blocks on the waves the band leaves idle (bands 2 and 3 keep only
+      // waves 0-1 / wave 0 busy): column block J needs Xd_0..Xd_J and U's rows above band J,
+      // all final once band J's F1 and barrier are past, so J = 0, 1 run beside band 2 and
+      // J = 2 beside band 3, and only J = 3 is left after the last band
+      const int jh = wv - 2;
+      int ln = lane;  // (opaque: keeps the lane-derived LDS addresses from being hoisted out
+      asm volatile("" : "+v"(ln));  // of the band loop, live across every elimination)
+      if (sb == 2) {
+        d2_inv_colhalf<1, SC1>(jh, S, Xd, winv, kb, ln);
+        d2_inv_colhalf<0, SC1>(jh, S, Xd, winv, kb, ln);
+      } else {
+        d2_inv_colhalf<2, SC1>(jh, S, Xd, winv, kb, ln);
+      }
     }
     __syncthreads();
     if (sb == 0) STAMP(5);
@@ -378,17 +393,11 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
       if (r < kb && c < kb && r <= c) st_res<SC1>(&Ab[(size_t)r + (size_t)c * lda], S[pk(r, c)]);
     }
   }
-  // W = U^-1, one wave per column half (MFMA work 144 / 144 / 112 / 112)
-  if (wv == 0) {
-    d2_inv_colhalf<3, SC1>(0, S, Xd, winv, kb, lane);
-  } else if (wv == 1) {
-    d2_inv_colhalf<3, SC1>(1, S, Xd, winv, kb, lane);
-  } else {
-    const int jh = wv - 2;
-    d2_inv_colhalf<2, SC1>(jh, S, Xd, winv, kb, lane);
-    d2_inv_colhalf<1, SC1>(jh, S, Xd, winv, kb, lane);
-    d2_inv_colhalf<0, SC1>(jh, S, Xd, winv, kb, lane);
-  }
+  // W = U^-1: the last column block, one wave per column half (blocks 0-2 went out beside
+  // bands 2 and 3).  In one phase here, waves 2-3 (blocks 2, 1, 0: 112 MFMAs and three
+  // halves' stores) ran 24.0k cycles against 15.3-17.6k for waves 0-1 (block 3: 144 MFMAs),
+  // tools/probe/inv_probe
+  if (wv < 2) d2_inv_colhalf<3, SC1>(wv, S, Xd, winv, kb, lane);
   STAMP(4);
   DSTAMP(7);
   return 0;

@@ -121,7 +121,7 @@ constexpr int DRPD = 64 / DNCH;             // rows per wave-wide 1-KB DMA
 constexpr int DNDMA = DT / (4 * DRPD);      // DMA instructions per wave per operand
 constexpr int DVM = 2 * DNDMA;              // vmcnt increments per stage
 constexpr int DNP = DTK / 8;                // fragment blocks (2 k-steps each) per stage
-static_assert(D2_LDS_DOUBLES <= DLDS, "diagonal block must fit in the stage buffers");
+static_assert(D2_LDS_QTAIL <= DLDS, "diagonal block must fit in the stage buffers");
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 
@@ -363,7 +363,7 @@ __device__ __attribute__((noinline)) int dag_factor(double* S, int mv, int kglob
   lds_d* L = (lds_d*)S;  // (one conversion; see diag_block.hpp)
   lds_d(*Xd)[D2_PB] = reinterpret_cast<lds_d(*)[D2_PB]>(L + D2_PK);
   lds_i* fail = reinterpret_cast<lds_i*>(L + D2_PK + 4 * D2_PB);
-  return diag2_core<true>(L, Xd, fail, nullptr, 0, mv, kglob, winv);
+  return diag2_core<true, true>(L, Xd, fail, nullptr, 0, mv, kglob, winv);
 }
 
 // (sc1: a launch hook's kernel reads U_ii on another stream while the launch runs -- a plain

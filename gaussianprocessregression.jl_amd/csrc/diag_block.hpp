@@ -97,12 +97,19 @@ constexpr int D2_PB = 32 * 33 / 2;              // packed 32x32 upper
 // 64-double pivot-row buffer (16-B aligned)
 constexpr int D2_PIV = D2_PK + 4 * D2_PB + 2;
 constexpr int D2_LDS_DOUBLES = D2_PIV + 4 * 64;
+// the tile-DAG's factor (QTAIL) also keeps W's off-diagonal blocks X_01, X_02, X_12 (32 x 33,
+// row-major) and the Q^T half-tiles the last column block's waves exchange
+constexpr int D2_XO = D2_LDS_DOUBLES;
+constexpr int D2_QS = D2_XO + 3 * 32 * 33;
+constexpr int D2_LDS_QTAIL = D2_QS + 3 * 2 * 4 * 64;
 
 // column half (J, jh) of W = U^-1 (see above); S = U packed upper (128), Xd = packed diag inverses
+// (Xo != nullptr: the off-diagonal blocks X_IJ also go to Xo[I + J - 1], row-major, stride 33)
 template <int J, bool SC1>
 __device__ __forceinline__ void d2_inv_colhalf(int jh, const lds_d* __restrict__ S,
                                                const lds_d (*__restrict__ Xd)[D2_PB],
-                                               double* __restrict__ winv, int kb, int lane) {
+                                               double* __restrict__ winv, int kb, int lane,
+                                               lds_d* __restrict__ Xo = nullptr) {
   d4v X[J + 1][2];
   const int col = 16 * jh + (lane & 15);  // column within block J
 #pragma unroll
@@ -142,6 +149,11 @@ __device__ __forceinline__ void d2_inv_colhalf(int jh, const lds_d* __restrict__
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(i <= m ? -xv : 0.0, T[st >> 2][st & 3], acc, 0, 0, 0);
       }
       X[I][ih] = acc;
+      if (Xo) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Xo[(I + J - 1) * 32 * 33 + (16 * ih + (lane >> 4) + 4 * r) * 33 + col] = acc[r];
+      }
     }
   }
   const int gc = 32 * J + col;
@@ -155,6 +167,82 @@ __device__ __forceinline__ void d2_inv_colhalf(int jh, const lds_d* __restrict__
         const double v = (I <= J) ? X[I <= J ? I : 0][ih][r] : 0.0;
         st_res<SC1>(&winv[gr + (size_t)gc * 128], (gr < kb && gc < kb) ? v : 0.0);
       }
+}
+
+// W's last column block without the recurrence's chain (the tile-DAG's factor): block column 3
+// of W U = I gives X_I3 = -Q_I Xd_3 with Q_I = sum_{K=I..2} X_IK U_K3 (X_II = Xd_I), so all
+// three row blocks are independent products.  Wave (H, ih) forms the Q^T half-tiles (H, I, ih)
+// (48 MFMAs: A = U_K3^T from S, B = X_IK^T from Xd / Xo) -- in D layout they are the B operands
+// of X_I3^T = -Xd_3^T Q_I^T directly -- the H = 0 waves pass theirs through Qs, and after one
+// barrier each wave writes the X_I3 tiles of its column half (4 (H + 1) MFMAs each) and its
+// X_33 tile: 48 + 24 MFMAs on the busiest wave against 144 dependent ones for a column half of
+// the recurrence.  The X_I3^T D layout stores 16 consecutive rows per column (128-B segments).
+// (two halves around the caller's barrier: the Q^T half-tiles, then the products and stores)
+template <int H>
+__device__ __forceinline__ void d2_tail_q(int ih, const lds_d* __restrict__ S,
+                                          const lds_d (*__restrict__ Xd)[D2_PB],
+                                          const lds_d* __restrict__ Xo, lds_d* __restrict__ Qs,
+                                          int lane, d4v (&q)[3]) {
+  const int n = 16 * ih + (lane & 15);  // row of block I (B operand column)
+#pragma unroll
+  for (int I = 0; I < 3; ++I) {
+    q[I] = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int K = I; K < 3; ++K)
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int k = 4 * st + (lane >> 4);
+        const double a = S[pk(32 * K + k, 96 + 16 * H + (lane & 15))];
+        double b;
+        if (K == I) {
+          const double v = Xd[I][pk(min(n, k), k)];
+          b = n <= k ? v : 0.0;
+        } else {
+          b = Xo[(I + K - 1) * 32 * 33 + n * 33 + k];
+        }
+        q[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, q[I], 0, 0, 0);
+      }
+  }
+  if constexpr (H == 0) {
+#pragma unroll
+    for (int I = 0; I < 3; ++I)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Qs[((I * 2 + ih) * 4 + r) * 64 + lane] = q[I][r];
+  }
+}
+
+template <int H, bool SC1>
+__device__ __forceinline__ void d2_tail_out(int ih, const lds_d (*__restrict__ Xd)[D2_PB],
+                                            const lds_d* __restrict__ Qs, const d4v (&q)[3],
+                                            double* __restrict__ winv, int kb, int lane) {
+  const int n = 16 * ih + (lane & 15);
+  const int c = 16 * H + (lane & 15);  // column of block 3 (A operand row)
+#pragma unroll
+  for (int I = 0; I < 3; ++I) {
+    d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int st = 0; st < 4 * (H + 1); ++st) {
+      const int m = 4 * st + (lane >> 4);
+      const double xv = Xd[3][pk(min(m, c), c)];
+      const double b = (st >> 2) == H ? q[I][st & 3] : Qs[((I * 2 + ih) * 4 + (st & 3)) * 64 + lane];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(m <= c ? -xv : 0.0, b, acc, 0, 0, 0);
+    }
+    const int gr = 32 * I + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gc = 96 + 16 * H + (lane >> 4) + 4 * r;
+      st_res<SC1>(&winv[gr + (size_t)gc * 128], (gr < kb && gc < kb) ? acc[r] : 0.0);
+    }
+  }
+  {  // X_33 = Xd_3 (zero below the diagonal)
+    const int gr = 96 + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int cc = 16 * H + (lane >> 4) + 4 * r, gc = 96 + cc;
+      const double v = Xd[3][pk(min(n, cc), cc)];
+      st_res<SC1>(&winv[gr + (size_t)gc * 128], (n <= cc && gr < kb && gc < kb) ? v : 0.0);
+    }
+  }
 }
 
 // S <- the upper triangle of the kb x kb block at Ab (identity padding beyond kb), packed.
@@ -186,7 +274,7 @@ __device__ __forceinline__ void diag2_load(lds_d* __restrict__ S, const double* 
 // the first non-positive pivot -- then U is not written (W's workspace slot may hold its first
 // column blocks).  Uniform across the workgroup.
 // Xd: 4 x D2_PB doubles of LDS; fail: one int of LDS.
-template <bool SC1>
+template <bool SC1, bool QTAIL = false>
 __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restrict__ Xd)[D2_PB],
                                           lds_i* fail, double* __restrict__ Ab, size_t lda, int kb,
                                           int kglob, double* __restrict__ winv) {
@@ -303,11 +391,12 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
       const int jh = wv - 2;
       int ln = lane;  // (opaque: keeps the lane-derived LDS addresses from being hoisted out
       asm volatile("" : "+v"(ln));  // of the band loop, live across every elimination)
+      lds_d* Xo = QTAIL ? S + D2_XO : nullptr;
       if (sb == 2) {
-        d2_inv_colhalf<1, SC1>(jh, S, Xd, winv, kb, ln);
+        d2_inv_colhalf<1, SC1>(jh, S, Xd, winv, kb, ln, Xo);
         d2_inv_colhalf<0, SC1>(jh, S, Xd, winv, kb, ln);
       } else {
-        d2_inv_colhalf<2, SC1>(jh, S, Xd, winv, kb, ln);
+        d2_inv_colhalf<2, SC1>(jh, S, Xd, winv, kb, ln, Xo);
       }
     }
     __syncthreads();
@@ -397,7 +486,20 @@ __device__ __forceinline__ int diag2_core(lds_d* __restrict__ S, lds_d (*__restr
   // bands 2 and 3).  In one phase here, waves 2-3 (blocks 2, 1, 0: 112 MFMAs and three
   // halves' stores) ran 24.0k cycles against 15.3-17.6k for waves 0-1 (block 3: 144 MFMAs),
   // tools/probe/inv_probe
-  if (wv < 2) d2_inv_colhalf<3, SC1>(wv, S, Xd, winv, kb, lane);
+  if constexpr (QTAIL) {  // wave (H, ih) = (wv / 2, wv % 2)
+    d4v q[3];
+    if (wv < 2)
+      d2_tail_q<0>(wv, S, Xd, S + D2_XO, S + D2_QS, lane, q);
+    else
+      d2_tail_q<1>(wv - 2, S, Xd, S + D2_XO, S + D2_QS, lane, q);
+    __syncthreads();  // the H = 0 half-tiles are in Qs
+    if (wv < 2)
+      d2_tail_out<0, SC1>(wv, Xd, S + D2_QS, q, winv, kb, lane);
+    else
+      d2_tail_out<1, SC1>(wv - 2, Xd, S + D2_QS, q, winv, kb, lane);
+  } else if (wv < 2) {
+    d2_inv_colhalf<3, SC1>(wv, S, Xd, winv, kb, lane);
+  }
   STAMP(4);
   DSTAMP(7);
   return 0;

@@ -81,7 +81,9 @@ __device__ __forceinline__ void st_res(double* p, double v) {
 // Inverse W = U^-1 from U and the Xd: column half (J, jh) of W is a 16-column recurrence
 //   X_JJ = Xd_J,  X_IJ = -Xd_I sum_{K=I+1..J} U_IK X_KJ   (I = J-1 .. 0)
 // kept entirely in MFMA accumulators (D-layout register q = B operand of k-step q), one
-// wave per column half; W goes to the workspace slot with fire-and-forget stores.  No
+// wave per column half -- blocks 0-1 beside band 2 and block 2 beside band 3 (waves 2-3, idle
+// there), block 3 after the last band (the tile-DAG's factor: in Q form on all four waves,
+// d2_tail_q / d2_tail_out); W goes to the workspace slot with fire-and-forget stores.  No
 // global read-back and no barrier after a global store, so nothing waits on HBM latency
 // except the single batched load of the block.
 __device__ __forceinline__ double readlane_d(double v, int lane) {

@@ -27,8 +27,15 @@ times, and `roofline` for the dominant kernel -- potrf_dag_kernel, the persisten
 launch that factors K and solves U^T [V | z] = [K(x, xp) | y] (N^3/3 + N^2 (np + 1) flops),
 or, with GPR_DAG=0, the pipelined FP64 MFMA GEMM of the blocked path -- measured with HIP
 events on the stream it runs on over one instrumented step; `cpu_baseline` = the CPU oracle
-(threaded C K-build + OpenBLAS LAPACK) on a bounded sample (N = 8192, np = 2048), scaled to
-the job.
+(threaded C K-build + OpenBLAS LAPACK) timed on the C3 job itself (N = 32768, np = 8192,
+median of 3 after a warm-up; --cpu-n / --cpu-np shrink it, and the stages are then scaled by
+their complexity to the job).
+
+Output: rank 0 prints the ONE JSON line on stdout as soon as the headline, its instrumented
+step and the CPU baseline are measured -- BEFORE the C5 leg, so a failure or hang inside the
+leg (RCCL across ranks) cannot cost the headline.  The C5 leg's own JSON object follows on
+stderr (key `split_predict`), and a watchdog ends the process if the leg outlives
+--split-timeout seconds.
 """
 from __future__ import annotations
 
@@ -80,11 +87,12 @@ def pmc_traffic(kernels, n, npred, largest=False):
             continue
         if largest:  # the job's launch of a kernel also launched with less work per call
             if all("traffic_bytes_max_launch" in k for k in ks):
-                return max(k["traffic_bytes_max_launch"] for k in ks)
+                return max(k["traffic_bytes_max_launch"] for k in ks), f"profiles/{f}"
             continue
         w = [k.get("trace", {}).get("calls") or k.get("dispatches_fetch_pass") or 1 for k in ks]
-        return sum(wi * k["traffic_bytes_per_launch"] for wi, k in zip(w, ks)) / sum(w)
-    return None
+        return (sum(wi * k["traffic_bytes_per_launch"] for wi, k in zip(w, ks)) / sum(w),
+                f"profiles/{f}")
+    return None, None
 
 
 def pmc_mfma(kernel, n, npred):
@@ -126,6 +134,9 @@ def parse():
     ap.add_argument("--no-split", action="store_true",
                     help="skip the C5 split-predict leg (extra key `split_predict`)")
     ap.add_argument("--split-steps", type=int, default=2)
+    ap.add_argument("--split-timeout", type=float, default=300.0,
+                    help="watchdog: end the process (exit 0, headline already printed) if the "
+                         "C5 leg runs longer than this many seconds")
     # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices by
     # LOCAL_RANK modulo the device count): gloo carries the collectives (RCCL refuses two
     # ranks on one device); the driver's runs use the default nccl (= RCCL), one rank per GPU
@@ -455,7 +466,7 @@ def main():
     achieved = g_fl / (g_ms * 1e-3) / 1e12 if g_ms > 0 else 0.0
     # the DAG kernel also runs alone (factorisation only) in the stage breakdown: its traffic
     # per JOB launch is the largest of the profiled launches
-    traffic = pmc_traffic(dominant, N, NP, largest=dominant == (DAG_KERNEL,))
+    traffic, traffic_src = pmc_traffic(dominant, N, NP, largest=dominant == (DAG_KERNEL,))
 
     out = None
     if rank == 0:
@@ -494,6 +505,13 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK,
                 "traffic": traffic,
+                # HBM bytes per launch: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE of the
+                # kernel's largest launch, from separate rocprofv3 --pmc passes of this command
+                # (tools/profile_round.sh), read from the newest committed summary -- not
+                # measured inside this run
+                "traffic_source": (f"{traffic_src} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                                   "passes of this bench command; not measured in this run)"
+                                   if traffic_src else None),
                 "launches": g_launch,
                 "avg_launch_us": g_ms * 1e3 / max(g_launch, 1),
                 "flops_per_launch": g_fl / max(g_launch, 1),
@@ -507,8 +525,30 @@ def main():
         if world > 1 and a.dist_backend == "gloo":
             out["rehearsal"] = (f"{world} ranks sharing {ndev} device(s) over gloo: plumbing "
                                 "check, not scaling data")
-    split = None
+    if rank == 0:
+        if not a.no_cpu_baseline and world == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline(a, kinds, hp)
+            except Exception as ex:  # never let the baseline leg kill the bench line
+                out["cpu_baseline"] = {"value": None, "error": repr(ex)}
+        else:
+            out["cpu_baseline"] = None
+        out["split_predict"] = ("skipped (--no-split)" if a.no_split else
+                                "C5 leg runs after this line; its JSON object is on stderr")
+        # the ONE stdout line, before the C5 leg: nothing in the leg can cost the headline
+        print(json.dumps(out), flush=True)
     if not a.no_split:
+        import threading
+
+        def _watchdog():  # a leg stuck in a collective: end the process, line already out
+            print(json.dumps({"split_predict": {"value": None, "error":
+                                                f"timed out after {a.split_timeout:.0f} s"}}),
+                  file=sys.stderr, flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(a.split_timeout, _watchdog)
+        wd.daemon = True
+        wd.start()
         try:
             with _StdoutToStderr():
                 if not dist.is_initialized():  # one rank: a 1-process RCCL group for C5
@@ -517,20 +557,13 @@ def main():
                     dist.init_process_group("nccl", rank=0, world_size=1,
                                             device_id=torch.device("cuda", local))
                 split = split_leg(a, dist.get_world_size(), rank, local)
-        except Exception as ex:  # never let the C5 leg kill the headline line
+        except Exception as ex:  # (reported, never raised: the headline is already out)
             # (split_predict_distributed exchanges a status before each data collective, so a
             # failure raises on every rank at the same point and no rank is left blocked)
             split = {"value": None, "error": repr(ex)}
-    if rank == 0:
-        out["split_predict"] = split
-        if not a.no_cpu_baseline and world == 1:
-            try:
-                out["cpu_baseline"] = cpu_baseline(a, kinds, hp)
-            except Exception as ex:  # never let the baseline leg kill the bench line
-                out["cpu_baseline"] = {"value": None, "error": repr(ex)}
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+        wd.cancel()
+        if rank == 0:
+            print(json.dumps({"split_predict": split}), file=sys.stderr, flush=True)
     if dist.is_initialized():
         with _StdoutToStderr():
             dist.barrier()

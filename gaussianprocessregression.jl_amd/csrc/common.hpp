@@ -100,6 +100,10 @@ struct gpr_ctx {
                    const int* ustored, int nt, hipEvent_t counters_reset) = nullptr;
   void* dag_hook_user = nullptr;
   int dag_reserve_cu = 0;  // CUs the persistent grid leaves free for such concurrent work
+  // set by a hook that left work polling dag_sync on another stream: the next DAG launch on
+  // this context waits for it before resetting (or reallocating) the counters
+  hipEvent_t dag_sync_readers = nullptr;
+  bool dag_sync_readers_pending = false;
   bool rhs_solved = false; // the last potrf_core solved its RhsSpec (not dropped by its block sizes)
   bool gram_full = false; // the last potrf_core wrote its RhsSpec gram in full (the tile-DAG)
   int dag_gram = 1;       // K^{-1} += Z^T Z as gram tile tasks of the DAG launch (GPR_DAG_GRAM)

@@ -765,8 +765,9 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     if (gram)
       for (int j = 0; j < nt; ++j)
         for (int i = 0; i <= j; ++i) tasks.push_back(((unsigned)i << 16) | (unsigned)j);
-    // a previous launch on this context may still be reading the old list (solves do not
-    // synchronise): drain the context's stream before freeing it
+    // a previous launch on this context may still be reading the old list (a factorisation
+    // launch returns without synchronising; a solve-only launch syncs to read its info, but
+    // the list may belong to a factorisation): drain the context's stream before freeing it
     if (ctx->dag_tasks) {
       HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (every DAG launch joins it)
       HIP_TRY(ctx, hipFree(ctx->dag_tasks));
@@ -781,6 +782,13 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_ntr = ntr;
     ctx->dag_flags = flags;
     ctx->dag_lag_built = (ctx->dag_zlag * 1024 + ctx->dag_rlag) * 2 + ctx->dag_fearly;
+  }
+  // a previous launch's hook may have left readers of the counters (row gates on another
+  // stream): they must drain before the counters are reset or reallocated
+  if (ctx->dag_sync_readers_pending) {
+    HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->dag_sync_readers, 0));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->dag_sync_readers, 0));
+    ctx->dag_sync_readers_pending = false;
   }
   // [2 + nt + ntr + i]: ustored[i] (hook launches; zeroed with the rest)
   const size_t nsync = 2 + (size_t)nt + ntr + nt;
@@ -855,7 +863,11 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     else
       potrf_dag_kernel<false><<<grid, 256, 0, st>>>(a);
     ctx->ls = ls;
-    LAUNCH_CHECK(ctx);
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess) {
+      if (hook_ev) hipEventDestroy(hook_ev);  // (the hook is not called: nothing was launched)
+      return set_err(ctx, GPR_E_HIP, "tile-DAG launch: %s", hipGetErrorString(le));
+    }
   }
   if (hook) {
     hook(ctx->dag_hook_user, dA, n, lda, ctx->dag_sync + 2, a.ustored, nt, hook_ev);

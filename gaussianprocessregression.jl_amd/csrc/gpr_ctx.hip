@@ -231,6 +231,10 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (!ctx) return 0;
   for (auto* sub : ctx->cv_sub) gpr_ctx_destroy(sub);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->dag_sync_readers) {  // a hook's readers of dag_sync (freed below)
+    hipEventSynchronize(ctx->dag_sync_readers);
+    hipEventDestroy(ctx->dag_sync_readers);
+  }
   drain_timing(ctx);
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto e : ctx->sync_events) hipEventDestroy(e);

@@ -21,8 +21,9 @@
 //   3. out  -- every device copies its rows of mu (ne x nq column-major, index e + q ne) and of
 //              the variance diagonal (index e nq + q) straight into the caller's host arrays
 //              (each GPU over its own PCIe link; no gather through one device).
-// One host thread per device drives phases 1-3 (each with the device current); the broadcast
-// is one RCCL group over all devices from the calling thread.  RCCL is loaded with dlopen, so
+// One host thread per device drives phases 1-3 (each with the device current) and issues its
+// own ungrouped RCCL calls on its communicator (no ncclGroupStart/End: each rank posts every
+// chunk's broadcast, in the same order, from its own thread).  RCCL is loaded with dlopen, so
 // libgpr_hip.so has no link-time dependency on it and a host process that already carries a
 // librccl.so.1 (torch) shares that one.
 #include <dlfcn.h>
@@ -47,8 +48,6 @@ struct RcclApi {
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
                             hipStream_t) = nullptr;
-  ncclResult_t (*GroupStart)() = nullptr;
-  ncclResult_t (*GroupEnd)() = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 
@@ -65,12 +64,9 @@ bool load_rccl(RcclApi* r, std::string* err) {
   r->CommInitAll = (decltype(r->CommInitAll))dlsym(h, "ncclCommInitAll");
   r->CommDestroy = (decltype(r->CommDestroy))dlsym(h, "ncclCommDestroy");
   r->Broadcast = (decltype(r->Broadcast))dlsym(h, "ncclBroadcast");
-  r->GroupStart = (decltype(r->GroupStart))dlsym(h, "ncclGroupStart");
-  r->GroupEnd = (decltype(r->GroupEnd))dlsym(h, "ncclGroupEnd");
   r->GetErrorString = (decltype(r->GetErrorString))dlsym(h, "ncclGetErrorString");
-  if (!r->CommInitAll || !r->CommDestroy || !r->Broadcast || !r->GroupStart || !r->GroupEnd ||
-      !r->GetErrorString) {
-    *err = "librccl.so.1 lacks an ncclCommInitAll / ncclBroadcast / ncclGroup* symbol";
+  if (!r->CommInitAll || !r->CommDestroy || !r->Broadcast || !r->GetErrorString) {
+    *err = "librccl.so.1 lacks an ncclCommInitAll / ncclCommDestroy / ncclBroadcast symbol";
     return false;
   }
   r->h = h;
@@ -268,17 +264,22 @@ struct StreamOut {
   long long limit = 1ll << 27;  // gate polls (~minutes: a gate waits up to a whole fit)
   bool fired = false;  // chunks enqueued by the hook, beside the DAG launch
   int rc = 0;
+  // fault injection (tests, GPR_MGPU_FAIL_UNPACK=k): every receiver's unpack of chunk k fails
+  // (skipped, error recorded, protocol continued) -- the self-broadcast receiver included
+  int fail_unpack = -1;
+  int recv_rc = 0;  // the self-broadcast receiver's error (device 0 reports it at the end)
 };
 
-// (dep: the event the chunks wait for -- the counters' reset, or the end of the fit)
+// (dep: the event the chunks wait for -- the counters' reset, or the end of the fit; null when
+// the caller has already synchronised with the fit)
 int enqueue_chunks(StreamOut* so, const int* colprog, const int* ustored, int nt, hipEvent_t dep) {
   gpr_mgpu* h = so->h;
   auto& R = h->rccl;
-  // every chunk's broadcast is issued even after a failed launch (the receivers are already
-  // waiting in the matching calls; the host reports the error afterwards) -- only a failing
-  // RCCL call ends the loop
+  // every chunk's broadcast is issued whatever fails on the way -- a failed launch, a failed
+  // RCCL call -- because the receivers are already waiting in the matching calls; the first
+  // error is returned after the last chunk and the host reports it
   int rc = 0;
-  if (hipStreamWaitEvent(h->sp, dep, 0) != hipSuccess) rc = GPR_E_HIP;
+  if (dep && hipStreamWaitEvent(h->sp, dep, 0) != hipSuccess) rc = GPR_E_HIP;
   for (size_t c = 0; c + 1 < so->rows.size(); ++c) {
     const int r0 = so->rows[c], r1 = so->rows[c + 1];
     double* slice = so->pk + rows_base(r0, so->n);
@@ -286,12 +287,16 @@ int enqueue_chunks(StreamOut* so, const int* colprog, const int* ustored, int nt
     if (colprog)
       rows_gate_kernel<<<1, 256, 0, h->sp>>>(colprog, ustored, nt, r0, r1, so->limit, h->derr);
     launch_rows_pack(h->sp, so->U, so->n, so->n, r0, r1, so->pk, true);
-    if (hipGetLastError() != hipSuccess) rc = GPR_E_HIP;
-    if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess) {
+    if (hipGetLastError() != hipSuccess && !rc) rc = GPR_E_HIP;
+    if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess && !rc)
       rc = GPR_E_HIP;
-      break;
+    if (so->U2 && !so->recv_rc) {  // the self-broadcast receiver's unpack
+      if ((int)c == so->fail_unpack)
+        so->recv_rc = GPR_E_HIP;
+      else
+        launch_rows_pack(h->sp, so->U2, so->n, so->n, r0, r1, so->pk, false);
+      if (hipGetLastError() != hipSuccess) so->recv_rc = GPR_E_HIP;
     }
-    if (so->U2) launch_rows_pack(h->sp, so->U2, so->n, so->n, r0, r1, so->pk, false);
   }
   return rc;
 }
@@ -305,6 +310,17 @@ void stream_out_hook(void* user, const double* dA, int n, int lda, const int* co
   if (!counters_reset || !ustored || dA != so->U || n != so->n || lda != so->n) return;
   so->rc = enqueue_chunks(so, colprog, ustored, nt, counters_reset);
   so->fired = true;
+  // the gates poll the launch's counters (ctx->dag_sync) on sp: the context's next DAG launch
+  // waits for them before it resets or reallocates that buffer
+  gpr_ctx* c = so->h->ctx[0];
+  if (!c->dag_sync_readers &&
+      hipEventCreateWithFlags(&c->dag_sync_readers, hipEventDisableTiming) != hipSuccess)
+    c->dag_sync_readers = nullptr;
+  if (c->dag_sync_readers && hipEventRecord(c->dag_sync_readers, so->h->sp) == hipSuccess)
+    c->dag_sync_readers_pending = true;
+  else if (hipStreamSynchronize(so->h->sp) != hipSuccess && !so->rc)  // (no event: drain now)
+    so->rc = GPR_E_HIP;
+  (void)hipGetLastError();
 }
 
 // run f(i) for every device on its own host thread (device i current), collect return codes
@@ -490,12 +506,14 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   }
   // Broadcast protocol (every device runs it in full, whatever happens to the fit, so no
   // receiver is left waiting in RCCL): chunks of tile rows of U in the row layout (about equal
-  // bytes, at most GPR_MGPU_CHUNKS = 16), then wt.  Streamed (default; GPR_MGPU_STREAM=0: after
-  // the fit): device 0's factorisation leaves GPR_MGPU_RESERVE_CU (8) CUs free and each chunk is
-  // packed and broadcast beside it as soon as its tile rows are final; the receivers unpack each
-  // chunk as it lands.  Only the last chunk and wt trail the factorisation.
+  // bytes, at most GPR_MGPU_CHUNKS = 16), then wt.  Streamed: device 0's factorisation leaves
+  // GPR_MGPU_RESERVE_CU (8) CUs free and each chunk is packed and broadcast beside it as soon as
+  // its tile rows are final; the receivers unpack each chunk as it lands, and only the last
+  // chunk and wt trail the factorisation.  GPR_MGPU_STREAM default: streamed on one device (the
+  // self-broadcast path the tests run), after the fit across devices -- no run with two or more
+  // GPUs has exercised the streamed receivers yet; GPR_MGPU_STREAM=1 opts in there.
   const char* e_st = getenv("GPR_MGPU_STREAM");
-  const bool stream = !e_st || atoi(e_st) != 0;
+  const bool stream = e_st ? atoi(e_st) != 0 : G == 1;
   const char* e_rs = getenv("GPR_MGPU_RESERVE_CU");
   const int reserve = e_rs ? std::max(0, atoi(e_rs)) : 8;
   const char* e_ch = getenv("GPR_MGPU_CHUNKS");
@@ -507,6 +525,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   // (tests: GPR_MGPU_GATE_LIMIT=0 makes every gate give up at once -- the error path whatever
   // the factorisation's progress)
   if (const char* e = getenv("GPR_MGPU_GATE_LIMIT")) so.limit = std::max(0ll, atoll(e));
+  if (const char* e = getenv("GPR_MGPU_FAIL_UNPACK")) so.fail_unpack = atoi(e);
   // 0. buffers and inputs on every device (a failure here stops every device before the
   //    broadcast protocol starts)
   auto rc = on_devices(h, [&](int i) -> int {
@@ -543,18 +562,34 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     auto& R = h->rccl;
     hipStream_t s = (hipStream_t)gpr_ctx_stream(c);
     if (i > 0) {  // receiver: every chunk, unpacked as it lands, then wt
+      // every broadcast is posted whatever fails (device 0 sends them all): after an error
+      // the remaining chunks are still received -- not unpacked -- and the error is reported
+      // once the protocol is complete, so neither side is left waiting in RCCL
+      int err = 0;
+      std::string what;
       for (size_t k = 0; k + 1 < so.rows.size(); ++k) {
         const int r0 = so.rows[k], r1 = so.rows[k + 1];
         double* slice = b.pk + rows_base(r0, ns);
         const size_t len = chunk_len(r0, r1, ns);
-        if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[i], s) != ncclSuccess)
-          return set_err(c, GPR_E_HIP, "RCCL broadcast of chunk %zu failed", k);
+        if (R.Broadcast(slice, slice, len, ncclDouble, 0, h->comm[i], s) != ncclSuccess) {
+          if (!err) err = GPR_E_HIP, what = "RCCL broadcast of chunk " + std::to_string(k);
+          continue;
+        }
+        if (err) continue;
+        if ((int)k == so.fail_unpack) {
+          err = GPR_E_HIP;
+          what = "unpack of chunk " + std::to_string(k) + " (injected: GPR_MGPU_FAIL_UNPACK)";
+          continue;
+        }
         launch_rows_pack(s, b.U, ns, ns, r0, r1, b.pk, false);
-        HIP_TRY(c, hipGetLastError());
+        if (hipGetLastError() != hipSuccess)
+          err = GPR_E_HIP, what = "unpack of chunk " + std::to_string(k);
       }
-      if (R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[i], s) != ncclSuccess)
-        return set_err(c, GPR_E_HIP, "RCCL broadcast of wt failed");
-      GPR_TRY(gpr_sync(c));
+      if (R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[i], s) != ncclSuccess && !err)
+        err = GPR_E_HIP, what = "RCCL broadcast of wt";
+      const int src = gpr_sync(c);
+      if (err) return set_err(c, err, "receiver: %s failed", what.c_str());
+      if (src) return src;
       return gpr_forget_factor(c);  // the inverses of this buffer's old contents are stale
     }
     // device 0: fit with the hook armed, then whatever the hook did not send, then wt
@@ -571,21 +606,34 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     c->dag_reserve_cu = 0;
     (void)hipGetLastError();  // (a failed fit must not stop the protocol below)
     int prc = so.fired ? so.rc : 0;
-    hipEvent_t fit_done = nullptr;  // wt (and, unless streamed, U) leave after the fit
-    if (hipEventCreateWithFlags(&fit_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventRecord(fit_done, s) != hipSuccess)
-      prc = GPR_E_HIP;
-    if (prc == 0 && !so.fired) prc = enqueue_chunks(&so, nullptr, nullptr, 0, fit_done);
-    if (prc == 0 && hipStreamWaitEvent(h->sp, fit_done, 0) != hipSuccess) prc = GPR_E_HIP;
-    if (prc == 0 && R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess)
+    // wt (and, unless streamed, U) leave after the fit: behind an event, or -- if none can be
+    // made -- after a host sync; the protocol runs to its end whatever failed
+    hipEvent_t fit_done = nullptr;
+    if (hipEventCreateWithFlags(&fit_done, hipEventDisableTiming) != hipSuccess) fit_done = nullptr;
+    if (fit_done && hipEventRecord(fit_done, s) != hipSuccess) {
+      hipEventDestroy(fit_done);
+      fit_done = nullptr;
+    }
+    if (!fit_done && hipStreamSynchronize(s) != hipSuccess && !prc) prc = GPR_E_HIP;
+    (void)hipGetLastError();
+    if (!so.fired) {
+      const int r2 = enqueue_chunks(&so, nullptr, nullptr, 0, fit_done);
+      if (!prc) prc = r2;
+    }
+    if (fit_done && hipStreamWaitEvent(h->sp, fit_done, 0) != hipSuccess && !prc) prc = GPR_E_HIP;
+    if (R.Broadcast(b.wt, b.wt, ns, ncclDouble, 0, h->comm[0], h->sp) != ncclSuccess && !prc)
       prc = GPR_E_HIP;
     if (fit_done) hipEventDestroy(fit_done);
-    if (hipStreamSynchronize(h->sp) != hipSuccess) prc = GPR_E_HIP;
+    if (hipStreamSynchronize(h->sp) != hipSuccess && !prc) prc = GPR_E_HIP;
+    c->dag_sync_readers_pending = false;  // (sp drained: the gates are done)
     if (r != 0) return r;
     if (prc != 0) return set_err(c, GPR_E_HIP, "device 0: streaming U / wt out failed");
     int herr = 0;
     HIP_TRY(c, hipMemcpy(&herr, h->derr, sizeof(int), hipMemcpyDeviceToHost));
     if (herr) return set_err(c, GPR_E_HIP, "device 0: a tile-row gate timed out");
+    if (so.recv_rc)
+      return set_err(c, so.recv_rc, "device 0 (self-broadcast receiver): unpack of chunk %d failed%s",
+                     so.fail_unpack, so.fail_unpack >= 0 ? " (injected: GPR_MGPU_FAIL_UNPACK)" : "");
     if (self_bcast) GPR_TRY(gpr_forget_factor(c));
     return gpr_sync(c);
   });

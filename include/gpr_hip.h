@@ -217,7 +217,7 @@ int gpr_antideriv_se(gpr_ctx_t ctx, int d, const double* hp, const double* dX, i
                      const double* a, const double* b, double* dk1, double* k2);
 /* integrate(md, hp, a, b; sample_noise=nothing) (src/integrate.jl:48-167): fit (K into dK ->
  * U, dwt = K^{-1} y, n x ny), Iout[ny] = wt' k1, *var = k2 - ||U^{-T} k1||^2 (host outputs).
- * The sample_noise path (symmetric eigendecomposition, :71-78) is not provided. */
+ * The sample_noise path (symmetric eigendecomposition, :71-78) is gpr_integrate_noise below. */
 int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                   const double* dX, int n, const double* dy, int ny, int ldy, const double* a,
                   const double* b, double eps, double* dK, int ldk, double* dwt, double* Iout,

@@ -542,3 +542,56 @@ def test_split_predict_mgpu_gate_timeout_reports_and_recovers(monkeypatch):
     mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 7))
     np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream,chunk", [("1", "0"), ("1", "3"), ("0", "2")])
+def test_split_predict_mgpu_unpack_failure_reports_and_recovers(monkeypatch, stream, chunk):
+    """A receiver whose unpack of one chunk fails (GPR_MGPU_FAIL_UNPACK=k, fault injection the
+    self-broadcast receiver honours) keeps receiving every remaining chunk and wt -- the sender
+    posts them all -- and reports the error once the protocol is complete: the call returns an
+    error instead of hanging, and the next call on the same handle is correct."""
+    G = pytest.importorskip("gpr_amd")
+    monkeypatch.setenv("GPR_MGPU_SELF_BCAST", "1")
+    monkeypatch.setenv("GPR_MGPU_STREAM", stream)
+    monkeypatch.setenv("GPR_MGPU_CHUNKS", "5")
+    kinds, hp, x, y, xe, xq = _problem(ne=7, nq=9, ns=4096, d=5, seed=14)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    mg = gd.MultiGPU([0])
+    try:
+        monkeypatch.setenv("GPR_MGPU_FAIL_UNPACK", chunk)
+        with pytest.raises(G.GprError, match=f"unpack of chunk {chunk} failed"):
+            gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
+        monkeypatch.delenv("GPR_MGPU_FAIL_UNPACK")
+        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
+    finally:
+        mg.close()
+    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 7))
+    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", ["0", "1"])
+def test_split_predict_mgpu_two_devices(monkeypatch, stream):
+    """gpr_split_predict_mgpu over two GPUs (the real receiver branch, RCCL between devices)
+    against the single-device split predict.  Skips on a box with fewer than two GPUs (the
+    development pool has one; no ngpu >= 2 run has happened yet)."""
+    G = pytest.importorskip("gpr_amd")
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    monkeypatch.setenv("GPR_MGPU_STREAM", stream)
+    kinds, hp, x, y, xe, xq = _problem(ne=11, nq=13, ns=2048, d=4, seed=15)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    mg = gd.MultiGPU([0, 1])
+    try:
+        for fit in ("broadcast", "replicate"):
+            mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(2, 11), fit=fit)
+            mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(2, 11))
+            np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
+            np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+    finally:
+        mg.close()

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <vector>
 
 #include "common.hpp"
 #include "kexp.hpp"
@@ -768,6 +769,165 @@ __global__ __launch_bounds__(256, 4) void kmat_crossg_kernel(KParams kp, const d
   }
 }
 
+// ---- upper-only K for a factorisation (the tile-DAG mirrors the rest) -------------------
+// Column c gets rows [0, min(n, 128 (c / 128 + 1))): the upper triangle plus the whole 128 x
+// 128 diagonal blocks -- everything the tile-DAG reads -- as ONE contiguous run per column;
+// the DAG stores each off-diagonal tile it loads, transposed, into the strict lower triangle
+// (DAG_MIRROR), so the buffer still ends as upper U / strict lower K with half the bytes here.
+// Work item = (strip of 32 columns, segment of 256 rows), one wave each, no LDS but the exp
+// tables and no barrier: the strip's column operands and norms stay in registers while the
+// wave walks down its segment 32 rows at a time.  The MFMA is oriented so that the D layout is
+// the store layout: operand A = column points, B = row points, so lane l, register q of block
+// (rb, cb) holds row i0 + 16 rb + (l & 15), column j0 + 16 cb + (l >> 4) + 4 q, and each store
+// instruction writes 4 columns x 128 contiguous bytes -- no LDS staging.  Elements of the
+// diagonal blocks are computed in both orientations, bitwise equal: (2 y_i) y_j and (2 y_j) y_i
+// are the same products, summed over the same k order from the same C = -|y_i|^2 - |y_j|^2.
+constexpr int KU_W = 32;   // strip width (columns) = unit edge
+#ifndef KU_MINB  // workgroups (of 4 independent waves) per CU the upper-only build is compiled for
+#define KU_MINB 3
+#endif
+constexpr int KU_SEG = 256;  // rows per work item
+
+// rows of column block j0 the factorisation reads
+__host__ __device__ inline int kup_rows(int j0, int n) { return min(n, 128 * (j0 / 128 + 1)); }
+
+// One 32 x 32 unit (rows i0.., columns j0..) of the upper-only build.  Per part: the four
+// blocks' MFMAs first (their latency overlaps the previous part's / unit's exponentials), then
+// the 16 exponentials per lane in groups of GRAM_EXPG.  DIAG: the unit on the diagonal (D = 0
+// and eps per part on i == j, sigma_n^2 after the parts); EDGE: rows past r1 / columns past n
+// masked.  Interior units store unconditionally, so the compiler counts the stores and the next
+// unit's prefetched operands are waited for with vmcnt(stores), not vmcnt(0).
+template <int S, int NSE, bool DIAG, bool EDGE>
+__device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[NSE][2][S],
+                                         const double* cn, const double (&ra)[NSE][2][S],
+                                         const double (&rn)[NSE][2], const double* tabs,
+                                         double* __restrict__ K, size_t ldk, int i0, int j0,
+                                         int r1, int n, int voff) {
+  const int lane = threadIdx.x & 63;
+  // block by block: its parts' MFMAs, then its 4 x NSE exponentials, then its 4 stores.  The
+  // empty asm statements pin each finished value where it is made: without them the compiler
+  // sank the second half of every exponential down to the stores and kept all 16 in flight
+  // (200+ registers, one wave per SIMD)
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      gd4 acc[NSE];
+#pragma unroll
+      for (int p = 0; p < NSE; ++p) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[p][q] = rn[p][rb] + cn[KU_W * p + 16 * cb + (lane >> 4) + 4 * q];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[p][cb][s], ra[p][rb][s], acc[p], 0, 0, 0);
+      }
+      double v[4];
+#pragma unroll
+      for (int p = 0; p < NSE; ++p) {
+        const double* ts = tabs + 256 * p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double x = acc[p][q];  // -D
+          bool on = false;
+          if (DIAG) {
+            on = rb == cb && (lane & 15) == (lane >> 4) + 4 * q;
+            if (on) x = 0.0;
+          }
+          double e = kexp_s2(-x, ts);
+          if (DIAG && on) e += kp.eps;
+          v[q] = p == 0 ? e : v[q] + e;
+          asm volatile("" : "+v"(v[q]));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double val = v[q];
+        if (DIAG && kp.has_noise && rb == cb && (lane & 15) == (lane >> 4) + 4 * q) val += kp.noise2;
+        // uniform base (SGPR) + the lane's 32-bit offset: rows 16 rb + (lane & 15), columns
+        // 16 cb + 4 q + (lane >> 4) of the unit
+        double* base = K + (size_t)(i0 + 16 * rb) + (size_t)(j0 + 16 * cb + 4 * q) * ldk;
+#ifdef GPR_KBUILD_NOSTORE  // diagnostics (tools/kbuild_bench_nostore): compute-only timing
+        if (!(val == val)) base[voff] = val;
+#else
+        if (!EDGE || (i0 + 16 * rb + (lane & 15) < r1 && j0 + 16 * cb + 4 * q + (lane >> 4) < n))
+          __builtin_nontemporal_store(val, base + voff);
+#endif
+      }
+    }
+}
+
+template <int S, int NSE>
+__global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, const double* __restrict__ gA,
+                                                        const double* __restrict__ gB,
+                                                        const double* __restrict__ nrm, int nblk,
+                                                        int n, double* __restrict__ K, size_t ldk,
+                                                        const int* __restrict__ items, int nitems) {
+  extern __shared__ double tabs[];  // NSE exp tables, then per wave the strip's column norms
+  load_part_tables(kp, tabs);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int W = gridDim.x * 4;
+  const int voff = (lane & 15) + (lane >> 4) * (int)ldk;  // (< 2^31: ldk < 2^29)
+  double* cn = tabs + 256 * NSE + (threadIdx.x >> 6) * (KU_W * NSE);  // this wave's
+  for (int t = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); t < nitems;
+       t += W) {
+    const int code = __builtin_amdgcn_readfirstlane(items[t]);
+    const int j0 = (code >> 16) * KU_W, r0 = (code & 0xffff) * KU_SEG;
+    const int r1 = min(r0 + KU_SEG, kup_rows(j0, n));
+    // the strip's column operands (A role, registers) and column norms (this wave's LDS: the
+    // lanes of a block read 4 distinct addresses per instruction -- broadcasts)
+    double ca[NSE][2][S];
+#pragma unroll
+    for (int p = 0; p < NSE; ++p)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int bb = (j0 >> 4) + cb;
+#pragma unroll
+        for (int s = 0; s < S; ++s) ca[p][cb][s] = gB[(((size_t)p * nblk + bb) * S + s) * 64 + lane];
+      }
+    __builtin_amdgcn_wave_barrier();  // (the previous item's norm reads are done: one wave)
+    if (lane < KU_W)
+#pragma unroll
+      for (int p = 0; p < NSE; ++p) cn[KU_W * p + lane] = nrm[(size_t)p * nblk * 16 + j0 + lane];
+    __builtin_amdgcn_wave_barrier();
+    // row operands (B role) of a 32-row unit: clamped to the last unit (branch-free prefetch)
+    auto load_rows = [&](int i0, double (&ra)[NSE][2][S], double (&rn)[NSE][2]) {
+      const int ii = min(i0, r1 - 1) & ~(KU_W - 1);
+#pragma unroll
+      for (int p = 0; p < NSE; ++p)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const int ba = (ii >> 4) + rb;
+#pragma unroll
+          for (int s = 0; s < S; ++s) ra[p][rb][s] = gA[(((size_t)p * nblk + ba) * S + s) * 64 + lane];
+          rn[p][rb] = nrm[(size_t)p * nblk * 16 + ba * 16 + (lane & 15)];
+        }
+    };
+    double ra[NSE][2][S], rn[NSE][2];
+    load_rows(r0, ra, rn);
+    const bool edge_cols = j0 + KU_W > n;
+    for (int i0 = r0; i0 < r1; i0 += KU_W) {
+      double nra[NSE][2][S], nrn[NSE][2];
+      load_rows(i0 + KU_W, nra, nrn);  // next unit's rows, in flight during this one
+      if (i0 == j0)  // (wave-uniform branches) the diagonal unit, ragged edges, the rest
+        kup_unit<S, NSE, true, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+      else if (edge_cols || i0 + KU_W > r1)
+        kup_unit<S, NSE, false, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+      else
+        kup_unit<S, NSE, false, false>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+#pragma unroll
+      for (int p = 0; p < NSE; ++p)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) ra[p][rb][s] = nra[p][rb][s];
+          rn[p][rb] = nrn[p][rb];
+        }
+    }
+  }
+}
+
 inline bool gram_enabled(int d) {
   static const bool exact = getenv("GPR_KBUILD_EXACT") != nullptr;
   return !exact && d <= 4 * 5;
@@ -816,6 +976,62 @@ int launch_gram(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const 
   }
   LAUNCH_CHECK(ctx);
   return 0;
+}
+
+// the upper-only build (kmat_symu_kernel): operands as launch_gram's same-object path
+template <int S, int NSE>
+int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk) {
+  const int d = kp.d;
+  const int nbA = ((n + KT - 1) / KT) * (KT / 16);
+  const size_t opA = (size_t)NSE * nbA * S * 64, nA = (size_t)NSE * nbA * 16;
+  GPR_TRY(ensure_buf(ctx, &ctx->dgc, &ctx->gc_cap, (size_t)KMAXP * KMAXD));
+  GPR_TRY(ensure_buf(ctx, &ctx->dgA, &ctx->gA_cap, 2 * opA + nA));
+  double* A = ctx->dgA;
+  double* nrmA = A + opA;
+  double* B = nrmA + nA;
+  if (ctx->kup_items_n != n) {  // work list: strip-major (bj << 16 | segment)
+    std::vector<int> items;
+    for (int bj = 0; bj * KU_W < n; ++bj) {
+      const int rows = kup_rows(bj * KU_W, n);
+      for (int sg = 0; sg * KU_SEG < rows; ++sg) items.push_back((bj << 16) | sg);
+    }
+    if (ctx->kup_items) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      HIP_TRY(ctx, hipFree(ctx->kup_items));
+      ctx->kup_items = nullptr;
+    }
+    ctx->kup_items_n = -1;
+    HIP_TRY(ctx, hipMalloc((void**)&ctx->kup_items, items.size() * sizeof(int)));
+    HIP_TRY(ctx, hipMemcpy(ctx->kup_items, items.data(), items.size() * sizeof(int),
+                           hipMemcpyHostToDevice));
+    ctx->kup_nitems = (int)items.size();
+    ctx->kup_items_n = n;
+  }
+  gram_center_kernel<<<NSE * d, 256, 0, ctx->stream>>>(xs, n, d, ctx->dgc);
+  {
+    const size_t total = opA;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    gram_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(xs, n, d, S, nbA, NSE, ctx->dgc, 2.0, A, nrmA);
+    gram_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(xs, n, d, S, nbA, NSE, ctx->dgc, 1.0, B, nullptr);
+  }
+  LAUNCH_CHECK(ctx);
+  static const int wgs = getenv("GPR_KBUILD_UWGS") ? atoi(getenv("GPR_KBUILD_UWGS")) : 8;
+  const int grid = std::max(1, std::min((ctx->kup_nitems + 3) / 4, 256 * wgs));
+  kmat_symu_kernel<S, NSE><<<grid, 256, sizeof(double) * (256 + 4 * KU_W) * NSE, ctx->stream>>>(
+      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, ctx->kup_items, ctx->kup_nitems);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+template <int NSE>
+int launch_gram_upper_s(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk) {
+  switch ((kp.d + 3) / 4) {
+    case 1: return launch_gram_upper<1, NSE>(ctx, kp, xs, n, K, ldk);
+    case 2: return launch_gram_upper<2, NSE>(ctx, kp, xs, n, K, ldk);
+    case 3: return launch_gram_upper<3, NSE>(ctx, kp, xs, n, K, ldk);
+    case 4: return launch_gram_upper<4, NSE>(ctx, kp, xs, n, K, ldk);
+    default: return launch_gram_upper<5, NSE>(ctx, kp, xs, n, K, ldk);
+  }
 }
 
 int launch_gram_any(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const double* xps,
@@ -884,6 +1100,7 @@ __global__ __launch_bounds__(256) void pair_kernel(int mode, int d, const double
 
 int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
                          const double* dXp, int m, int same, double* dK, int ldk) {
+  if (dK == ctx->kup_ptr) ctx->kup_ptr = nullptr;  // (rebuilt in full)
   if (n <= 0 || (!same && m <= 0)) return 0;
   GPR_TRY(scale_inputs(ctx, kp, dX, n, &ctx->dxs, &ctx->xs_cap));
   if (same) {
@@ -902,6 +1119,29 @@ int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int 
     DISPATCH_D(launch_cross, ctx, kp, ctx->dxs, n, ctx->dxps, m, dK, ldk);
     LAUNCH_CHECK(ctx);
   }
+  return 0;
+}
+
+int launch_kernel_matrix_for_factor(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
+                                    double* dK, int ldk) {
+  ctx->kup_ptr = nullptr;
+  // upper-only where the tile-DAG will take exactly this matrix directly (potrf_core), with
+  // the Gram form (d <= 20) and one or two SE parts; the full symmetric K otherwise
+  const bool upper = ctx->kbuild_upper && n > 0 && gram_enabled(kp.d) && kp.nse <= 2 &&
+                     dag_takes_whole(ctx, n, ldk, dK) && dag_shape_ok(n, ldk, dK);
+  if (!upper) return launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk);
+  GPR_TRY(scale_inputs(ctx, kp, dX, n, &ctx->dxs, &ctx->xs_cap));
+  {
+    // bytes written: column c gets min(n, 128 (c / 128 + 1)) rows
+    double bytes = 0.0;
+    for (int c0 = 0; c0 < n; c0 += 128) bytes += 8.0 * std::min(128, n - c0) * kup_rows(c0, n);
+    TimerScope ts(ctx, TC_KBUILD, bytes);  // ("flops" slot: bytes written)
+    GPR_TRY(kp.nse == 1 ? launch_gram_upper_s<1>(ctx, kp, ctx->dxs, n, dK, ldk)
+                        : launch_gram_upper_s<2>(ctx, kp, ctx->dxs, n, dK, ldk));
+  }
+  ctx->kup_ptr = dK;
+  ctx->kup_n = n;
+  ctx->kup_ld = ldk;
   return 0;
 }
 

@@ -172,6 +172,15 @@ struct gpr_ctx {
   size_t gB_cap = 0;
   double* dgc = nullptr;        // Gram-assembly centres (KMAXP x KMAXD)
   size_t gc_cap = 0;
+  // upper-only K assembly for a factorisation (assembly.hip kmat_symu_kernel): its work list
+  // (strip << 16 | segment, built once per n) and the matrix it last left without its strict
+  // lower off-diagonal tiles -- the next potrf_core on exactly that matrix has the tile-DAG
+  // write them (DAG_MIRROR), or mirrors them first on any other path
+  int* kup_items = nullptr;
+  int kup_items_n = -1, kup_nitems = 0;
+  const double* kup_ptr = nullptr;
+  int kup_n = 0, kup_ld = 0;
+  int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)
 
   bool timing = false;
   std::vector<TimedLaunch> pending;
@@ -248,6 +257,13 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class);
 
 int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
                          const double* dXp, int m, int same, double* dK, int ldk);
+// K for a factorisation that follows at once (potrf_core on exactly dK): where the tile-DAG
+// takes the matrix directly, only what the factorisation reads is assembled -- the upper
+// triangle and the whole 128 x 128 diagonal blocks, column-contiguously -- and the DAG writes
+// the strict lower off-diagonal tiles from the tiles it loads (DAG_MIRROR); anything else
+// gets the full symmetric K.  The buffer ends as the reference's: upper U, strict lower K.
+int launch_kernel_matrix_for_factor(gpr_ctx* ctx, const KParams& kp, const double* dX, int n,
+                                    double* dK, int ldk);
 int launch_mirror_upper(gpr_ctx* ctx, double* A, int n, int lda);
 int launch_scale_inputs(gpr_ctx* ctx, const KParams& kp, const double* dX, int n, double* out);
 int launch_pair(gpr_ctx* ctx, int mode, int d, const double* xa, int na, const double* xb, int nb,
@@ -270,7 +286,10 @@ struct RhsSpec {
 };
 // one-launch tile-DAG factorisation (+ B <- U^{-T} B); 1 = shape not eligible, 0 = launched
 // DAG_GRAM (with DAG_LOWER, B = the identity's Z = U^{-T}): also G = Z^T Z (every tile)
-enum { DAG_SOLVE = 1, DAG_LOWER = 2, DAG_GRAM = 4 };
+// DAG_MIRROR: A holds only its upper triangle and 128 x 128 diagonal blocks (the upper-only
+// K assembly): every off-diagonal task also stores its loaded tile A_ij, transposed, into the
+// strict lower tile (j, i)
+enum { DAG_SOLVE = 1, DAG_LOWER = 2, DAG_GRAM = 4, DAG_MIRROR = 8 };
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
                      int kglob, hipStream_t st, int flags = 0, double* dG = nullptr, int ldg = 0);
 // true when potrf_core would factor (n, lda, dA) as ONE tile-DAG launch (directly, or for

@@ -146,6 +146,7 @@ struct DagArgs {
   size_t ldg;    // K^{-1} = Z^T Z; tickets >= gbase are these tiles
   int gbase;
   long long spin_limit;  // polls before a wait gives up (~4 s at 2^25; GPR_DAG_SPIN_LIMIT, tests)
+  int mirror;  // DAG_MIRROR: off-diagonal tasks store their loaded A_ij, transposed, at (j, i)
 };
 
 __device__ __forceinline__ int ld_sc1(const int* p) {
@@ -518,6 +519,23 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
             acc[ii][jj][r] = (mm < mv && nn < nv) ? -c : 0.0;
           }
         }
+      // DAG_MIRROR: the K assembly left the strict lower triangle to this launch -- the loaded
+      // tile, transposed, into tile (j, i) (K there, as dpotrf 'U' leaves it).  Lanes with one
+      // (lane & 15) store 32 contiguous bytes of one column per register r; the four r fill a
+      // 128-B line, which the L2 merges before writing back.  Nothing in the launch reads it.
+      if (a.mirror && !rhs && !diag) {
+        double* Tm = a.A + (size_t)j * DT + (size_t)i * DT * a.lda;
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int nn = wn * 64 + ii * 16 + (lane >> 4) + 4 * r;
+              const int mm = wm * 64 + jj * 16 + (lane & 15);
+              if (mm < mv && nn < nv) Tm[(size_t)nn + (size_t)mm * a.lda] = -acc[ii][jj][r];
+            }
+      }
       // acc += sum_{k<i} U_ki^T X_kj, row blocks taken as soon as both columns have them final
       DTRACE(1, 2);
       int done = (rhs && a.lower) ? j : 0;
@@ -589,6 +607,14 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
               if (mm < mv && nn < nv) st_res<true>(&T[(size_t)mm + (size_t)nn * ldt], acc[ii][jj][r]);
             }
           }
+      }
+    } else if (a.mirror && !rhs && !diag) {
+      // a skipped task (a pivot failed: dpotrf stops there) still owes the strict lower tile
+      // its K values -- its own upper tile was written by no one, so it still holds A_ij
+      double* Tm = a.A + (size_t)j * DT + (size_t)i * DT * a.lda;
+      for (int e = tid; e < DT * DT; e += 256) {
+        const int mm = e & (DT - 1), nn = e >> 7;
+        if (mm < mv && nn < nv) Tm[(size_t)nn + (size_t)mm * a.lda] = T[(size_t)mm + (size_t)nn * ldt];
       }
     }
     DTRACE(1, 5);
@@ -722,7 +748,9 @@ int launch_potrf_dag_padded(gpr_ctx* ctx, double* dA, int n, int lda, double* dB
 int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs, int ldb,
                      int kglob, hipStream_t st, int flags, double* dG, int ldg) {
   const bool solve = flags & DAG_SOLVE, lower = flags & DAG_LOWER, gram = flags & DAG_GRAM;
+  const bool mirror = flags & DAG_MIRROR;
   if ((solve || lower) && (!dB || kglob)) return 1;
+  if (mirror && (solve || kglob)) return 1;
   if (gram && (!lower || !dG || ldg < n || nrhs != n)) return 1;
   if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || ((uintptr_t)dA & 127) || n > DT * 32767 ||
       kglob % DT)
@@ -730,7 +758,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   if (dB && (nrhs <= 0 || ldb % 16 || ((uintptr_t)dB & 127) || nrhs > DT * 65535)) return 1;
   const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
   GPR_TRY(ensure_winv(ctx, kglob + n, DT));
-  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != flags ||
+  if (ctx->dag_nt != nt || ctx->dag_ntr != ntr || ctx->dag_flags != (flags & ~DAG_MIRROR) ||
       ctx->dag_lag_built != (ctx->dag_zlag * 1024 + ctx->dag_rlag) * 2 + ctx->dag_fearly) {
     std::vector<unsigned> tasks;
     tasks.reserve((size_t)nt * (nt + 1) + (size_t)nt * ntr);
@@ -780,7 +808,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->dag_ntasks = (int)tasks.size();
     ctx->dag_nt = nt;
     ctx->dag_ntr = ntr;
-    ctx->dag_flags = flags;
+    ctx->dag_flags = flags & ~DAG_MIRROR;  // (the task list does not depend on it)
     ctx->dag_lag_built = (ctx->dag_zlag * 1024 + ctx->dag_rlag) * 2 + ctx->dag_fearly;
   }
   // a previous launch's hook may have left readers of the counters (row gates on another
@@ -831,6 +859,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   a.G = gram ? dG : nullptr;
   a.ldg = (size_t)(gram ? ldg : 0);
   a.gbase = gram ? ctx->dag_ntasks - nt * (nt + 1) / 2 : ctx->dag_ntasks;
+  a.mirror = mirror;
   // (re-read per launch: the timeout tests shorten it around one call)
   const char* sl = getenv("GPR_DAG_SPIN_LIMIT");
   a.spin_limit = sl ? std::max(1ll, atoll(sl)) : ctx->dag_spin_limit;

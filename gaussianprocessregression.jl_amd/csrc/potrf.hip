@@ -1629,6 +1629,11 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   const int nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
   ctx->fac_valid = false;
   ctx->sqinv_nb2 = 0;
+  // dA as the upper-only K assembly left it (launch_kernel_matrix_for_factor): its strict lower
+  // off-diagonal tiles are written by the tile-DAG launch (DAG_MIRROR) or, on any other path,
+  // mirrored here before the factorisation overwrites the upper triangle
+  bool mirror = ctx->kup_ptr == dA && ctx->kup_n == n && ctx->kup_ld == lda;
+  ctx->kup_ptr = nullptr;
   GPR_TRY(ensure_winv(ctx, n, nb));
   if (rhs && (nb != 128 || nb2 > 2048 || !ctx->srhs || rhs->nrhs <= 0)) rhs = nullptr;
   ctx->rhs_solved = rhs != nullptr;  // (callers solve a dropped right-hand side afterwards)
@@ -1649,8 +1654,14 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
       rc = launch_potrf_dag(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
                             rhs ? rhs->ldb : 0, 0, ctx->stream,
                             (rhs && rhs->lower_rhs ? DAG_LOWER : 0) |
-                                (rhs && rhs->gram ? DAG_GRAM : 0),
+                                (rhs && rhs->gram ? DAG_GRAM : 0) | (mirror ? DAG_MIRROR : 0),
                             rhs ? rhs->gram : nullptr, rhs ? rhs->ldg : 0);
+    if (rc < 0) return rc;
+    if (rc == 0) mirror = false;  // (the launch writes the lower tiles)
+    if (mirror) {
+      GPR_TRY(launch_mirror_upper(ctx, dA, n, lda));
+      mirror = false;
+    }
     if (rc == 1 && (!rhs || !rhs->lower_rhs))
       rc = launch_potrf_dag_padded(ctx, dA, n, lda, rhs ? rhs->B : nullptr, rhs ? rhs->nrhs : 0,
                                    rhs ? rhs->ldb : 0);
@@ -1674,6 +1685,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
       return 0;
     }
   }
+  if (mirror) GPR_TRY(launch_mirror_upper(ctx, dA, n, lda));
   hipStream_t user = ctx->stream;
   ctx->gram_full = false;
   if (rhs && rhs->gram)  // accumulated panel by panel below (upper; the caller mirrors)

@@ -249,7 +249,7 @@ int gpr_fit(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d, co
   GPR_TRY(make_kparams(ctx, kinds, nk, hp, d, eps, &kp, nullptr));
   if (n <= 0 || ldk < n || nrhs <= 0 || ldy < n || !dX || !dy || !dK || !dalpha)
     return set_err(ctx, GPR_E_ARG, "bad args");
-  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  GPR_TRY(launch_kernel_matrix_for_factor(ctx, kp, dX, n, dK, ldk));
   HIP_TRY(ctx, hipMemcpy2DAsync(dalpha, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
                                 (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));
   int hinfo = 0;
@@ -317,7 +317,7 @@ int gpr_fit_kinv(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
   if (n <= 0 || ldk < n || ldkinv < n || nrhs <= 0 || ldy < n || !dX || !dy || !dK || !dalpha ||
       !dKinv)
     return set_err(ctx, GPR_E_ARG, "bad args");
-  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  GPR_TRY(launch_kernel_matrix_for_factor(ctx, kp, dX, n, dK, ldk));
   GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, (size_t)n * n));
   double* Z = ctx->dbig;
   GPR_TRY(launch_set_identity(ctx, Z, n, n));
@@ -391,7 +391,7 @@ int gpr_fit_predict(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
     W = ctx->dbig2;
   }
   double* Z = W + (size_t)n * m;
-  GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk));
+  GPR_TRY(launch_kernel_matrix_for_factor(ctx, kp, dX, n, dK, ldk));
   GPR_TRY(launch_cross_or_same(ctx, kp, dX, n, dXp, m, W));
   HIP_TRY(ctx, hipMemcpy2DAsync(Z, (size_t)n * sizeof(double), dy, (size_t)ldy * sizeof(double),
                                 (size_t)n * sizeof(double), nrhs, hipMemcpyDeviceToDevice, ctx->stream));

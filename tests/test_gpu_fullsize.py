@@ -96,6 +96,48 @@ def test_c3_fit_and_posterior_full_size():
     assert var.min() >= -1e-8 * prior and var.max() <= prior * (1 + 1e-8)
 
 
+def test_c3_fit_buffer_full_size():
+    """The bench's own call at C3 (gpr_fit_predict: upper-only K assembly, the tile-DAG writing
+    the strict lower tiles from the tiles it loads) leaves K's buffer exactly as the full
+    symmetric build (gpr_kernel) factored by gpr_potrf_upper does -- upper U, strict lower K,
+    the reference's cholesky!(Hermitian(K)) buffer (test/test_loss.jl:46) -- bit for
+    bit over all 32768^2 entries; sampled strict-lower entries equal the oracle's K."""
+    import ctypes
+    N, d, NP = 32768, 8, 8192
+    kinds = ["SE", "SE", "WN"]
+    hp = _hp(kinds, d)
+    x, y, xp = O.synthetic(d, N, NP)
+    ctx = G.Context(0)
+    lib = G._lib.lib
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    karr = (ctypes.c_int * 3)(1, 1, 2)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    dx, dy, dxp = ctx.colmajor(x), ctx.colmajor(y), ctx.colmajor(xp)
+    K1 = ctx.empty(N, N)
+    alpha, mu, var = ctx.empty(N), ctx.empty(NP), ctx.empty(NP)
+    W = ctx.empty(NP + 1, N)
+    info = ctypes.c_int(-7)
+    assert lib.gpr_fit_predict(ctx.h, karr, 3, hpp, d, P(dx), N, P(dy), 1, N, 1e-8, P(K1), N,
+                               P(alpha), P(dxp), NP, 1, P(mu), P(var), NP, P(W),
+                               ctypes.byref(info)) == 0 and info.value == 0
+    del W
+    K2 = ctx.empty(N, N)
+    assert lib.gpr_kernel(ctx.h, karr, 3, hpp, d, P(dx), N, None, N, 1, 1e-8, P(K2), N) == 0
+    # strict lower (tensor row c = column c: entries k > c of row c) against the oracle
+    rng = np.random.default_rng(11)
+    a = rng.integers(0, N, 256)
+    b = rng.integers(0, N, 256)
+    i, j = np.maximum(a, b), np.minimum(a, b)   # row i > column j: strict lower
+    keep = i > j
+    i, j = i[keep], j[keep]
+    got = K1[torch.from_numpy(j).to(K1.device), torch.from_numpy(i).to(K1.device)].cpu().numpy()
+    want = np.array([O.kernel(kinds, hp, x[:, [ii]], x[:, [jj]])[0, 0] for ii, jj in zip(i, j)])
+    np.testing.assert_allclose(got, want, rtol=1e-13, atol=0)
+    assert lib.gpr_potrf_upper(ctx.h, P(K2), N, N, ctypes.byref(info)) == 0 and info.value == 0
+    ctx.sync()
+    assert torch.equal(K1, K2)
+
+
 def test_c4_mll_and_gradient_full_size():
     N, d = 16384, 16
     kinds = ["SE", "WN"]

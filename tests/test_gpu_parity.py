@@ -1043,3 +1043,125 @@ def test_fit_kinv(n, nb2, fuse, monkeypatch):
     Ki = ctx.host(Kinv)
     assert np.array_equal(Ki, Ki.T)
     assert relnorm(Ki, O.kinv_from_upper(Uo)) < 1e-10
+
+
+# ---------------------------------------------------------------------------------------
+# Upper-only K assembly for a factorisation + the tile-DAG's lower mirror (round 4): the fit
+# buffer must still end as the reference's cholesky!(Hermitian(K)) leaves it -- upper U,
+# strict lower K (test/test_loss.jl:46 compares whole cache buffers) -- and equal,
+# bit for bit, the full symmetric build (gpr_kernel) factored by gpr_potrf_upper.
+# ---------------------------------------------------------------------------------------
+def _P(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _karr(kinds):
+    return (ctypes.c_int * len(kinds))(*[1 if k == SE else 2 for k in kinds])
+
+
+def _ref_buffer(ctx, kinds, hp, x, eps=1e-8):
+    """gpr_kernel (full symmetric K, GPR_SELF) + gpr_potrf_upper on a second buffer."""
+    d, n = x.shape
+    dx = ctx.colmajor(x)
+    K = ctx.empty(n, n)
+    karr = _karr(kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    assert G._lib.lib.gpr_kernel(ctx.h, karr, len(kinds), hpp, d, _P(dx), n, None, n, 1, eps,
+                                 _P(K), n) == 0
+    Kfull = ctx.host(K).copy()
+    info = ctypes.c_int(-7)
+    assert G._lib.lib.gpr_potrf_upper(ctx.h, _P(K), n, n, ctypes.byref(info)) >= 0
+    return ctx.host(K), Kfull, info.value
+
+
+@pytest.mark.parametrize("name", ["SE", "SE+WN", "SE+SE+WN", "SE+SE"])
+@pytest.mark.parametrize("n,dim", [(128, 3), (144, 8), (1040, 8), (2064, 5), (4096, 8), (1024, 16)])
+@pytest.mark.parametrize("call", ["fit", "fit_predict", "fit_kinv"])
+def test_fit_buffer_upper_build_dag_mirror(name, n, dim, call):
+    kinds = KSETS[name]
+    rng = np.random.default_rng(n + dim)
+    hp = O.default_hp(kinds, dim, noise=0.1)
+    x = rng.random((dim, n))
+    y = np.sin(x.sum(0)) ** 2
+    ctx = G.Context(0)
+    Rref, Kfull, info_ref = _ref_buffer(ctx, kinds, hp, x)
+    assert info_ref == 0
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, alpha = ctx.empty(n, n), ctx.empty(n)
+    karr = _karr(kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    info = ctypes.c_int(-7)
+    lib = G._lib.lib
+    if call == "fit":
+        rc = lib.gpr_fit(ctx.h, karr, len(kinds), hpp, dim, _P(dx), n, _P(dy), 1, n, 1e-8, _P(K), n,
+                         _P(alpha), ctypes.byref(info))
+    elif call == "fit_predict":
+        m = 37
+        xp = rng.random((dim, m))
+        dxp = ctx.colmajor(xp)
+        mu, var, W = ctx.empty(m), ctx.empty(m), ctx.empty(m + 1, n)
+        rc = lib.gpr_fit_predict(ctx.h, karr, len(kinds), hpp, dim, _P(dx), n, _P(dy), 1, n, 1e-8,
+                                 _P(K), n, _P(alpha), _P(dxp), m, 1, _P(mu), _P(var), m, _P(W),
+                                 ctypes.byref(info))
+    else:
+        Kinv = ctx.empty(n, n)
+        rc = lib.gpr_fit_kinv(ctx.h, karr, len(kinds), hpp, dim, _P(dx), n, _P(dy), 1, n, 1e-8, _P(K),
+                              n, _P(alpha), _P(Kinv), n, ctypes.byref(info))
+    assert rc == 0 and info.value == 0, lib.gpr_last_error(ctx.h)
+    R = ctx.host(K)
+    assert np.array_equal(R, Rref)                       # the whole buffer, bit for bit
+    assert np.array_equal(np.tril(R, -1), np.tril(Kfull, -1))
+    Ko = O.kernel(kinds, hp, x, None)
+    np.testing.assert_allclose(np.tril(R, -1), np.tril(Ko, -1), rtol=1e-13, atol=1e-300)
+    assert relnorm(np.triu(R), sla.cholesky(Ko, lower=False)) < 1e-11
+
+
+@pytest.mark.parametrize("env", [("GPR_DAG_GRAM", "0"), ("GPR_KBUILD_UPPER", "0")])
+def test_fit_buffer_upper_build_other_paths(env, monkeypatch):
+    """The upper-only build with a factorisation the DAG does not take as one launch
+    (gpr_fit_kinv with GPR_DAG_GRAM=0: the blocked path, which mirrors the strict lower first)
+    and with the upper-only build switched off: the same buffer as the full build."""
+    monkeypatch.setenv(*env)
+    kinds = KSETS["SE+WN"]
+    dim, n = 6, 1536
+    rng = np.random.default_rng(3)
+    hp = O.default_hp(kinds, dim, noise=0.1)
+    x = rng.random((dim, n))
+    y = np.sin(x.sum(0)) ** 2
+    ctx = G.Context(0)
+    Rref, Kfull, _ = _ref_buffer(ctx, kinds, hp, x)
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, alpha, Kinv = ctx.empty(n, n), ctx.empty(n), ctx.empty(n, n)
+    karr = _karr(kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    info = ctypes.c_int(-7)
+    rc = G._lib.lib.gpr_fit_kinv(ctx.h, karr, 2, hpp, dim, _P(dx), n, _P(dy), 1, n, 1e-8, _P(K), n,
+                                 _P(alpha), _P(Kinv), n, ctypes.byref(info))
+    assert rc == 0 and info.value == 0
+    R = ctx.host(K)
+    assert np.array_equal(np.tril(R, -1), np.tril(Kfull, -1))
+    assert relnorm(np.triu(R), np.triu(Rref)) < 1e-12
+
+
+@pytest.mark.parametrize("eps,fails_at", [(-0.012, 625), (-1.1, 1)])
+def test_fit_buffer_not_posdef_keeps_lower_k(eps, fails_at):
+    """A failing pivot (info > 0): the tasks after it skip their arithmetic, but the strict lower
+    triangle still ends as K everywhere (dpotrf leaves it untouched), as with the full build."""
+    kinds = KSETS["SE+WN"]
+    dim, n = 4, 1024
+    x, y, _ = O.synthetic(dim, n, 0, seed_train=3)
+    hp = O.default_hp(kinds, dim, noise=0.1)
+    ctx = G.Context(0)
+    Ko = O.kernel(kinds, hp, x, None, eps=eps)
+    _, info_ref = sla.lapack.dpotrf(Ko, lower=0)
+    assert info_ref == fails_at
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    K, alpha = ctx.empty(n, n), ctx.empty(n)
+    karr = _karr(kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    info = ctypes.c_int(-7)
+    rc = G._lib.lib.gpr_fit(ctx.h, karr, 2, hpp, dim, _P(dx), n, _P(dy), 1, n, eps, _P(K), n,
+                            _P(alpha), ctypes.byref(info))
+    assert rc == info.value == fails_at
+    _, Kfull, _ = _ref_buffer(ctx, kinds, hp, x, eps=eps)
+    assert np.array_equal(np.tril(ctx.host(K), -1), np.tril(Kfull, -1))

@@ -5,8 +5,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 #include "../include/gpr_hip.h"
+#include "../gaussianprocessregression.jl_amd/csrc/common.hpp"  // (upper-only build, internal)
 
 // write-bandwidth ceiling references: plain 16-B/lane streaming stores
 __global__ void store16_kernel(double* p, size_t n2) {
@@ -275,6 +277,25 @@ int main(int argc, char** argv) {
       printf("kbuild %-9s %s N=%d M=%d d=%d: %.3f ms  %.0f GB/s (%.1f%% of 8 TB/s)\n", c.name,
              cross ? "cross" : "sym  ", N, cross ? M : N, d, best, bytes / best / 1e6,
              bytes / best / 1e6 / 80.0);
+    }
+    {  // the fit paths' upper-only build (column c: rows [0, min(N, 128 (c/128 + 1))))
+      KParams kp;
+      if (make_kparams(ctx, c.kinds.data(), (int)c.kinds.size(), hp.data(), d, 1e-8, &kp, nullptr)) return 1;
+      float best = 1e30f;
+      for (int rep = 0; rep < 6; ++rep) {
+        hipEventRecord(e0, s);
+        int rc = launch_kernel_matrix_for_factor(ctx, kp, dx, N, K, (int)ld);
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        if (rc) { printf("rc=%d %s\n", rc, gpr_last_error(ctx)); return 1; }
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best = ms < best ? ms : best;
+      }
+      ctx->kup_ptr = nullptr;
+      double bytes = 0.0;
+      for (int c0 = 0; c0 < N; c0 += 128) bytes += 8.0 * std::min(128, N - c0) * std::min(N, c0 + 128);
+      printf("kbuild %-9s upper N=%d d=%d: %.3f ms  %.0f GB/s (%.1f%% of 8 TB/s) [%.2f GB written]\n",
+             c.name, N, d, best, bytes / best / 1e6, bytes / best / 1e6 / 80.0, bytes / 1e9);
     }
   }
   gpr_ctx_destroy(ctx);

@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--d", type=int, default=8)
     ap.add_argument("--ne", type=int, default=1024)
     ap.add_argument("--nq", type=int, default=1024)
-    ap.add_argument("--var-rows", type=int, default=32)
+    ap.add_argument("--var-rows", type=int, default=32,
+                    help="variance for grid rows 1..var_rows (the reference's var_range; "
+                         "SURVEY 8d: default 1:3 for parity, full 1:ne = 1024 for throughput)")
     ap.add_argument("--fit", default="broadcast", choices=["broadcast", "replicate"])
     return ap.parse_args()
 
@@ -78,16 +80,30 @@ def main():
     def step():
         return split_predict_distributed(md, cm, var_range=vr, fit=a.fit)
 
+    import ctypes
+    from gpr_amd import _lib
+    lib = _lib.lib
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     dist.barrier()
+    # per-launch HIP-event timing on the context's stream: timing class 7 = the solve-only
+    # tile-DAG launches (V = U^{-T} Kxq of the variance rows, nq ns^2 flops per grid row),
+    # class 6 = the fit's factorisation launch (not the timed quantity here)
+    lib.gpr_timing_reset(ctx.h)
+    lib.gpr_timing_enable(ctx.h, 1)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         mu, var = step()
     torch.cuda.synchronize()
     dist.barrier()
     dt = (time.perf_counter() - t0) / a.steps
+    lib.gpr_timing_enable(ctx.h, 0)
+    cls = {}
+    for c, nm in ((6, "dag_fit"), (7, "dag_solve")):
+        ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        lib.gpr_timing_get(ctx.h, c, ctypes.byref(ms), ctypes.byref(ln), ctypes.byref(fl))
+        cls[nm] = (ms.value, ln.value, fl.value)
     tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
@@ -112,6 +128,18 @@ def main():
                                    f"var_rows={a.var_rows} fit={a.fit}",
                        "parallelism": f"e-row shards x{world}, RCCL broadcast + all_gather"},
             "algorithmic_tflop_per_step": (mean_flops + var_flops) / 1e12,
+            # the variance solve (rank 0's solve-only tile-DAG launches, HIP events on the
+            # stream they run on): nq ns^2 flops per grid row, against the FP64 matrix peak
+            "var_solve": ({"kernel": "potrf_dag_kernel (solve-only launches)", "bound": "mfma",
+                           "launches": cls["dag_solve"][1],
+                           "avg_launch_ms": cls["dag_solve"][0] / cls["dag_solve"][1],
+                           "flops_per_launch": cls["dag_solve"][2] / cls["dag_solve"][1],
+                           "achieved_TFLOPs": cls["dag_solve"][2] / cls["dag_solve"][0] / 1e9,
+                           "peak_TFLOPs": 78.6,
+                           "frac": cls["dag_solve"][2] / cls["dag_solve"][0] / 1e9 / 78.6,
+                           "ms_per_step": cls["dag_solve"][0] / a.steps}
+                          if cls["dag_solve"][1] else None),
+            "fit_dag_ms_per_step": cls["dag_fit"][0] / a.steps,
             "results_finite": bool(np.isfinite(mu).all() and np.isfinite(var).all()),
         })
         os.write(json_fd, (line + "\n").encode())

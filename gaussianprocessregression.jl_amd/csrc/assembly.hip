@@ -787,6 +787,7 @@ constexpr int KU_W = 32;   // strip width (columns) = unit edge
 #define KU_MINB 3
 #endif
 constexpr int KU_SEG = 256;  // rows per work item
+constexpr double KU_NC_LIM = 1.4e6;  // |y|^2 below which the exponentials need no clamp
 
 // rows of column block j0 the factorisation reads
 __host__ __device__ inline int kup_rows(int j0, int n) { return min(n, 128 * (j0 / 128 + 1)); }
@@ -797,7 +798,7 @@ __host__ __device__ inline int kup_rows(int j0, int n) { return min(n, 128 * (j0
 // and eps per part on i == j, sigma_n^2 after the parts); EDGE: rows past r1 / columns past n
 // masked.  Interior units store unconditionally, so the compiler counts the stores and the next
 // unit's prefetched operands are waited for with vmcnt(stores), not vmcnt(0).
-template <int S, int NSE, bool DIAG, bool EDGE>
+template <int S, int NSE, bool DIAG, bool EDGE, bool CLAMP>
 __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[NSE][2][S],
                                          const double* cn, const double (&ra)[NSE][2][S],
                                          const double (&rn)[NSE][2], const double* tabs,
@@ -834,7 +835,7 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
             on = rb == cb && (lane & 15) == (lane >> 4) + 4 * q;
             if (on) x = 0.0;
           }
-          double e = kexp_s2(-x, ts);
+          double e = CLAMP ? kexp_s2(-x, ts) : kexp_s2_nc(-x, ts);
           if (DIAG && on) e += kp.eps;
           v[q] = p == 0 ? e : v[q] + e;
           asm volatile("" : "+v"(v[q]));
@@ -862,7 +863,8 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
                                                         const double* __restrict__ gB,
                                                         const double* __restrict__ nrm, int nblk,
                                                         int n, double* __restrict__ K, size_t ldk,
-                                                        const int* __restrict__ items, int nitems) {
+                                                        const int* __restrict__ items, int nitems,
+                                                        int full) {
   extern __shared__ double tabs[];  // NSE exp tables, then per wave the strip's column norms
   load_part_tables(kp, tabs);
   __syncthreads();
@@ -874,7 +876,7 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
        t += W) {
     const int code = __builtin_amdgcn_readfirstlane(items[t]);
     const int j0 = (code >> 16) * KU_W, r0 = (code & 0xffff) * KU_SEG;
-    const int r1 = min(r0 + KU_SEG, kup_rows(j0, n));
+    const int r1 = min(r0 + KU_SEG, full ? n : kup_rows(j0, n));
     // the strip's column operands (A role, registers) and column norms (this wave's LDS: the
     // lanes of a block read 4 distinct addresses per instruction -- broadcasts)
     double ca[NSE][2][S];
@@ -887,9 +889,17 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
         for (int s = 0; s < S; ++s) ca[p][cb][s] = gB[(((size_t)p * nblk + bb) * S + s) * 64 + lane];
       }
     __builtin_amdgcn_wave_barrier();  // (the previous item's norm reads are done: one wave)
+    // the exponentials skip their range clamp where D = |y_i|^2 + |y_j|^2 - 2 y_i.y_j <=
+    // 2 (|y_i|^2 + |y_j|^2) < 5.6e6 provably (kexp_s2_nc): every |y|^2 < KU_NC_LIM here
+    bool big = false;
     if (lane < KU_W)
 #pragma unroll
-      for (int p = 0; p < NSE; ++p) cn[KU_W * p + lane] = nrm[(size_t)p * nblk * 16 + j0 + lane];
+      for (int p = 0; p < NSE; ++p) {
+        const double c = nrm[(size_t)p * nblk * 16 + j0 + lane];
+        cn[KU_W * p + lane] = c;
+        big |= !(-c < KU_NC_LIM);
+      }
+    const bool cols_big = __ballot(big) != 0;
     __builtin_amdgcn_wave_barrier();
     // row operands (B role) of a 32-row unit: clamped to the last unit (branch-free prefetch)
     auto load_rows = [&](int i0, double (&ra)[NSE][2][S], double (&rn)[NSE][2]) {
@@ -910,12 +920,19 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
     for (int i0 = r0; i0 < r1; i0 += KU_W) {
       double nra[NSE][2][S], nrn[NSE][2];
       load_rows(i0 + KU_W, nra, nrn);  // next unit's rows, in flight during this one
-      if (i0 == j0)  // (wave-uniform branches) the diagonal unit, ragged edges, the rest
-        kup_unit<S, NSE, true, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+      bool rbig = cols_big;
+#pragma unroll
+      for (int p = 0; p < NSE; ++p) rbig |= !(-rn[p][0] < KU_NC_LIM) || !(-rn[p][1] < KU_NC_LIM);
+      const bool clamp = __ballot(rbig) != 0;
+      // (wave-uniform branches) the diagonal unit, ragged edges, the interior
+      if (i0 == j0)
+        kup_unit<S, NSE, true, true, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
       else if (edge_cols || i0 + KU_W > r1)
-        kup_unit<S, NSE, false, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+        kup_unit<S, NSE, false, true, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+      else if (clamp)
+        kup_unit<S, NSE, false, false, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
       else
-        kup_unit<S, NSE, false, false>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
+        kup_unit<S, NSE, false, false, false>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
 #pragma unroll
       for (int p = 0; p < NSE; ++p)
 #pragma unroll
@@ -980,7 +997,8 @@ int launch_gram(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const 
 
 // the upper-only build (kmat_symu_kernel): operands as launch_gram's same-object path
 template <int S, int NSE>
-int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk) {
+int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk,
+                      int full) {
   const int d = kp.d;
   const int nbA = ((n + KT - 1) / KT) * (KT / 16);
   const size_t opA = (size_t)NSE * nbA * S * 64, nA = (size_t)NSE * nbA * 16;
@@ -989,10 +1007,10 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
   double* A = ctx->dgA;
   double* nrmA = A + opA;
   double* B = nrmA + nA;
-  if (ctx->kup_items_n != n) {  // work list: strip-major (bj << 16 | segment)
+  if (ctx->kup_items_n != 2 * n + full) {  // work list: strip-major (bj << 16 | segment)
     std::vector<int> items;
     for (int bj = 0; bj * KU_W < n; ++bj) {
-      const int rows = kup_rows(bj * KU_W, n);
+      const int rows = full ? n : kup_rows(bj * KU_W, n);
       for (int sg = 0; sg * KU_SEG < rows; ++sg) items.push_back((bj << 16) | sg);
     }
     if (ctx->kup_items) {
@@ -1005,7 +1023,7 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
     HIP_TRY(ctx, hipMemcpy(ctx->kup_items, items.data(), items.size() * sizeof(int),
                            hipMemcpyHostToDevice));
     ctx->kup_nitems = (int)items.size();
-    ctx->kup_items_n = n;
+    ctx->kup_items_n = 2 * n + full;
   }
   gram_center_kernel<<<NSE * d, 256, 0, ctx->stream>>>(xs, n, d, ctx->dgc);
   {
@@ -1018,19 +1036,20 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
   static const int wgs = getenv("GPR_KBUILD_UWGS") ? atoi(getenv("GPR_KBUILD_UWGS")) : 8;
   const int grid = std::max(1, std::min((ctx->kup_nitems + 3) / 4, 256 * wgs));
   kmat_symu_kernel<S, NSE><<<grid, 256, sizeof(double) * (256 + 4 * KU_W) * NSE, ctx->stream>>>(
-      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, ctx->kup_items, ctx->kup_nitems);
+      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, ctx->kup_items, ctx->kup_nitems, full);
   LAUNCH_CHECK(ctx);
   return 0;
 }
 
 template <int NSE>
-int launch_gram_upper_s(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk) {
+int launch_gram_upper_s(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, double* K, int ldk,
+                        int full) {
   switch ((kp.d + 3) / 4) {
-    case 1: return launch_gram_upper<1, NSE>(ctx, kp, xs, n, K, ldk);
-    case 2: return launch_gram_upper<2, NSE>(ctx, kp, xs, n, K, ldk);
-    case 3: return launch_gram_upper<3, NSE>(ctx, kp, xs, n, K, ldk);
-    case 4: return launch_gram_upper<4, NSE>(ctx, kp, xs, n, K, ldk);
-    default: return launch_gram_upper<5, NSE>(ctx, kp, xs, n, K, ldk);
+    case 1: return launch_gram_upper<1, NSE>(ctx, kp, xs, n, K, ldk, full);
+    case 2: return launch_gram_upper<2, NSE>(ctx, kp, xs, n, K, ldk, full);
+    case 3: return launch_gram_upper<3, NSE>(ctx, kp, xs, n, K, ldk, full);
+    case 4: return launch_gram_upper<4, NSE>(ctx, kp, xs, n, K, ldk, full);
+    default: return launch_gram_upper<5, NSE>(ctx, kp, xs, n, K, ldk, full);
   }
 }
 
@@ -1107,6 +1126,12 @@ int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int 
     const double el = (double)n * n;
     TimerScope ts(ctx, TC_KBUILD, el * 8.0);  // "flops" slot carries algorithmic bytes
     // (the Gram kernels store 16-B pairs: 16-B aligned K with an even ldk, else difference form)
+    // one SE part: both halves computed by the column build (store-bound: one exponential per
+    // element is cheaper than the mirrored tiles' store pattern); more parts: upper tiles
+    // computed once and mirrored through LDS (the exponentials dominate)
+    if (gram_enabled(kp.d) && kp.nse <= std::min(ctx->kbuild_full_cols_nse, 2))
+      return kp.nse == 1 ? launch_gram_upper_s<1>(ctx, kp, ctx->dxs, n, dK, ldk, 1)
+                         : launch_gram_upper_s<2>(ctx, kp, ctx->dxs, n, dK, ldk, 1);
     if (gram_enabled(kp.d) && vec_store_ok(dK, ldk))
       return launch_gram_any(ctx, kp, ctx->dxs, n, nullptr, n, 1, dK, ldk);
     DISPATCH_D(launch_sym, ctx, kp, ctx->dxs, n, dK, ldk);
@@ -1136,8 +1161,8 @@ int launch_kernel_matrix_for_factor(gpr_ctx* ctx, const KParams& kp, const doubl
     double bytes = 0.0;
     for (int c0 = 0; c0 < n; c0 += 128) bytes += 8.0 * std::min(128, n - c0) * kup_rows(c0, n);
     TimerScope ts(ctx, TC_KBUILD, bytes);  // ("flops" slot: bytes written)
-    GPR_TRY(kp.nse == 1 ? launch_gram_upper_s<1>(ctx, kp, ctx->dxs, n, dK, ldk)
-                        : launch_gram_upper_s<2>(ctx, kp, ctx->dxs, n, dK, ldk));
+    GPR_TRY(kp.nse == 1 ? launch_gram_upper_s<1>(ctx, kp, ctx->dxs, n, dK, ldk, 0)
+                        : launch_gram_upper_s<2>(ctx, kp, ctx->dxs, n, dK, ldk, 0));
   }
   ctx->kup_ptr = dK;
   ctx->kup_n = n;

@@ -32,7 +32,7 @@ struct KParams {
 // site), recorded in addition to the call-site class.
 enum TimingClass {
   TC_KBUILD = 0, TC_SYRK = 1, TC_PANEL = 2, TC_TRSM_GEMM = 3, TC_OTHER = 4, TC_GEMM_PIPE = 5,
-  TC_DAG = 6, TC_N = 7
+  TC_DAG = 6, TC_DAG_SOLVE = 7, TC_N = 8
 };
 
 struct TimedLaunch {
@@ -180,7 +180,11 @@ struct gpr_ctx {
   int kup_items_n = -1, kup_nitems = 0;
   const double* kup_ptr = nullptr;
   int kup_n = 0, kup_ld = 0;
+  double* deig = nullptr;       // block-Jacobi eigensolver workspace (eigen.hip)
+  size_t eig_cap = 0;
   int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)
+  int kbuild_full_cols_nse = 1; // full symmetric K by the column build (both halves computed)
+                                // for up to this many SE parts (GPR_KBUILD_FULLCOLS; 0: off)
 
   bool timing = false;
   std::vector<TimedLaunch> pending;
@@ -304,6 +308,10 @@ int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu);
 int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int nrhs,
                  int ldb, double* norm_out, int lower_rhs);
 int kinv_from_z(gpr_ctx* ctx, const double* Z, int n, double* dKinv, int ldk);
+// symmetric eigendecomposition A = P diag(lam) P^T applied to B: lam (n, device) and
+// B <- P^T B (n x m, ld ldb), A read only (eigen.hip, block Jacobi); *sweeps may be null
+int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                  double* dlam, int* sweeps);
 // norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream
 int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm);
 // forward = false: only the backward sweep U x = B (B already holds U^{-T} b);

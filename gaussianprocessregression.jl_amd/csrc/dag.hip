@@ -886,7 +886,7 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   {
     hipStream_t ls = ctx->ls;
     ctx->ls = st;  // TimerScope records on ctx->ls
-    TimerScope ts(ctx, TC_DAG, flops);
+    TimerScope ts(ctx, solve ? TC_DAG_SOLVE : TC_DAG, flops);  // (solve-only launches apart)
     if (gram)
       potrf_dag_kernel<true><<<grid, 256, 0, st>>>(a);
     else

@@ -1,0 +1,324 @@
+// Symmetric eigendecomposition applied to right-hand sides, hand-written for gfx950: the
+// sample_noise branch of Bayesian quadrature (src/integrate.jl:71-100, LAPACK.syevr! at :75)
+// needs lambda = eig(K) and P^T [Y | k1] only -- never P itself.
+//
+// Method: two-sided BLOCK Jacobi with a parallel (round-robin) ordering.  K (padded to a
+// multiple of 64 with zero rows/columns, which stay decoupled) is split into 32-wide blocks;
+// a round pairs every block with another (the circle method: nb - 1 rounds per sweep meet
+// every pair once).  Per round:
+//   1. one workgroup per pair (I, J) diagonalises its 64 x 64 subproblem S = K[I u J, I u J]
+//      in LDS by scalar parallel Jacobi (32 disjoint rotations per step, 63 steps per sweep,
+//      until a sweep rotates nothing) and writes the accumulated rotation R (64 x 64);
+//   2. every 64 x 64 tile of K in pair coordinates becomes R_k^T K[P_k, P_l] R_l (computed for
+//      k <= l and mirrored, so K stays exactly symmetric) and the pair's rows of B become
+//      R_k^T B[P_k, :] -- all pairs' transforms at once, J^T K J with J = diag(R_k).
+// A sweep that rotates nothing anywhere ends it: lambda = diag(K), B = P^T B_in.  Rotations
+// follow Rutishauser's stable formulas and are skipped when |s_pq| <= 1e-15 sqrt(|s_pp s_qq|)
+// (the Demmel-Veselic criterion: eigenvalues of a positive definite K to high relative
+// accuracy) or when the angle is below rounding (|tan| < 1e-17), so a converged matrix is
+// left exactly as it is (R = I is applied exactly).
+//
+// Cost: per round one small latency-bound launch (nb/2 workgroups) and one pass over K
+// (16 n^2 bytes, 2 x 64^3 FMAs per tile on the VALU, register-blocked 4 x 4 per thread);
+// nb - 1 rounds per sweep, ~6-10 sweeps.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int EB = 32;        // Jacobi block width
+constexpr int ES = 2 * EB;    // subproblem / tile edge
+constexpr int ELD = ES + 1;   // LDS row stride (doubles) of a 64 x 64 image
+
+// circle method over m slots (m even): round r pairs slot 0 with L[0] and L[i] with L[m-1-i],
+// L = (1..m-1) rotated by r
+__device__ __forceinline__ void circle_pair(int m, int r, int k, int* a, int* b) {
+  const int mm = m - 1;
+  auto L = [&](int i) { return (i + r) % mm + 1; };
+  if (k == 0) {
+    *a = 0;
+    *b = L(0);
+  } else {
+    *a = L(k);
+    *b = L(mm - k);
+  }
+}
+
+// global index of pair-local row i (0..63) of pair (I, J)
+__device__ __forceinline__ int pair_row(int I, int J, int i) {
+  return i < EB ? EB * I + i : EB * J + (i - EB);
+}
+
+// 1. per pair: diagonalise S = A[P, P] by parallel Jacobi in LDS, R = accumulated rotation
+__global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __restrict__ A, size_t lda,
+                                                            int nb, int round,
+                                                            double* __restrict__ Rbuf,
+                                                            int* __restrict__ rotations,
+                                                            int max_inner) {
+  __shared__ double S[ES * ELD];
+  __shared__ double R[ES * ELD];
+  __shared__ double cs[ES / 2][2];
+  __shared__ int pr[ES / 2][2];
+  __shared__ int rot_sweep, rot_total;
+  const int k = blockIdx.x, t = threadIdx.x;
+  int I, J;
+  circle_pair(nb, round, k, &I, &J);
+  for (int e = t; e < ES * ES; e += 256) {
+    const int i = e % ES, j = e / ES;
+    S[i + j * ELD] = A[(size_t)pair_row(I, J, i) + (size_t)pair_row(I, J, j) * lda];
+    R[i + j * ELD] = i == j ? 1.0 : 0.0;
+  }
+  if (t == 0) rot_total = 0;
+  __syncthreads();
+  for (int sweep = 0; sweep < max_inner; ++sweep) {
+    if (t == 0) rot_sweep = 0;
+    __syncthreads();
+    for (int step = 0; step < ES - 1; ++step) {
+      if (t < ES / 2) {
+        int p, q;
+        circle_pair(ES, step, t, &p, &q);
+        if (p > q) { const int w = p; p = q; q = w; }
+        const double app = S[p + p * ELD], aqq = S[q + q * ELD], apq = S[p + q * ELD];
+        double c = 1.0, s = 0.0;
+        if (apq != 0.0 && fabs(apq) > 1e-15 * sqrt(fabs(app * aqq))) {
+          // Rutishauser: theta = (aqq - app) / (2 apq), t = sign(theta) / (|theta| + sqrt(1 + theta^2))
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(1.0 + theta * theta));
+          if (fabs(tt) >= 1e-17) {
+            c = 1.0 / sqrt(1.0 + tt * tt);
+            s = tt * c;
+            atomicAdd(&rot_sweep, 1);
+          }
+        }
+        cs[t][0] = c;
+        cs[t][1] = s;
+        pr[t][0] = p;
+        pr[t][1] = q;
+      }
+      __syncthreads();
+      // rows p, q of S: S <- J^T S   (J: c at (p,p), (q,q); s at (p,q); -s at (q,p))
+      for (int e = t; e < (ES / 2) * ES; e += 256) {
+        const int pk = e / ES, j = e % ES;
+        const double c = cs[pk][0], s = cs[pk][1];
+        if (s == 0.0) continue;
+        const int p = pr[pk][0], q = pr[pk][1];
+        const double sp = S[p + j * ELD], sq = S[q + j * ELD];
+        S[p + j * ELD] = c * sp - s * sq;
+        S[q + j * ELD] = s * sp + c * sq;
+      }
+      __syncthreads();
+      // columns p, q of S and of R: S <- S J, R <- R J
+      for (int e = t; e < (ES / 2) * ES; e += 256) {
+        const int pk = e / ES, i = e % ES;
+        const double c = cs[pk][0], s = cs[pk][1];
+        if (s == 0.0) continue;
+        const int p = pr[pk][0], q = pr[pk][1];
+        const double sp = S[i + p * ELD], sq = S[i + q * ELD];
+        S[i + p * ELD] = c * sp - s * sq;
+        S[i + q * ELD] = s * sp + c * sq;
+        const double rp = R[i + p * ELD], rq = R[i + q * ELD];
+        R[i + p * ELD] = c * rp - s * rq;
+        R[i + q * ELD] = s * rp + c * rq;
+      }
+      __syncthreads();
+    }
+    const int rs = rot_sweep;
+    if (t == 0) rot_total += rs;
+    __syncthreads();  // (every thread has read rot_sweep before thread 0 resets it)
+    if (rs == 0) break;
+  }
+  double* Rk = Rbuf + (size_t)k * ES * ES;
+  for (int e = t; e < ES * ES; e += 256) Rk[e] = R[(e % ES) + (e / ES) * ELD];
+  if (t == 0 && rot_total) atomicAdd(rotations, rot_total);
+}
+
+// C (64 x 64, LDS stride ELD) = op(X)^T-or-not ... : thread t computes the 4 x 4 block
+// rows 4 (t % 16).., columns 4 (t / 16)..  of  C = TA ? X^T Y : X Y  (X, Y in LDS, stride ELD)
+template <bool TA>
+__device__ __forceinline__ void gemm64(const double* X, const double* Y, double (&c)[4][4]) {
+  const int t = threadIdx.x, i0 = 4 * (t % 16), j0 = 4 * (t / 16);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) c[a][b] = 0.0;
+  for (int kk = 0; kk < ES; ++kk) {
+    double x[4], y[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) x[a] = TA ? X[kk + (i0 + a) * ELD] : X[(i0 + a) + kk * ELD];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) y[b] = Y[kk + (j0 + b) * ELD];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) c[a][b] = fma(x[a], y[b], c[a][b]);
+  }
+}
+
+// 2. A[P_k, P_l] <- R_k^T A[P_k, P_l] R_l for every tile k <= l (mirrored into (l, k)), and
+//    B[P_k, cols] <- R_k^T B[P_k, cols] for every pair k and 64-column chunk of B
+__global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__ A, size_t lda,
+                                                           int nb, int round,
+                                                           const double* __restrict__ Rbuf,
+                                                           double* __restrict__ B, size_t ldb,
+                                                           int m, int ntiles) {
+  __shared__ double lds[4 * ES * ELD];  // 133 KB: one workgroup per CU
+  double* T = lds;               // tile (then U = T R_l)
+  double* Rl = T + ES * ELD;
+  double* Rk = Rl + ES * ELD;
+  double* U = Rk + ES * ELD;
+  const int t = threadIdx.x, np = nb / 2;
+  const int i0 = 4 * (t % 16), j0 = 4 * (t / 16);
+  int bid = blockIdx.x;
+  if (bid < ntiles) {
+    // tile (k, l), k <= l, from the linear upper-triangle index
+    int l = (int)((sqrt(8.0 * bid + 1.0) - 1.0) * 0.5);
+    while ((l + 1) * (l + 2) / 2 <= bid) ++l;
+    while (l * (l + 1) / 2 > bid) --l;
+    const int k = bid - l * (l + 1) / 2;
+    int Ik, Jk, Il, Jl;
+    circle_pair(nb, round, k, &Ik, &Jk);
+    circle_pair(nb, round, l, &Il, &Jl);
+    const double* Rkg = Rbuf + (size_t)k * ES * ES;
+    const double* Rlg = Rbuf + (size_t)l * ES * ES;
+    for (int e = t; e < ES * ES; e += 256) {
+      const int i = e % ES, j = e / ES;
+      T[i + j * ELD] = A[(size_t)pair_row(Ik, Jk, i) + (size_t)pair_row(Il, Jl, j) * lda];
+      Rl[i + j * ELD] = Rlg[e];
+      Rk[i + j * ELD] = Rkg[e];
+    }
+    __syncthreads();
+    double c[4][4];
+    gemm64<false>(T, Rl, c);  // U = T R_l
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) U[(i0 + a) + (j0 + b) * ELD] = c[a][b];
+    __syncthreads();
+    gemm64<true>(Rk, U, c);   // R_k^T U
+    if (k == l) {             // exactly symmetric: the upper half, mirrored
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) T[(i0 + a) + (j0 + b) * ELD] = c[a][b];
+      __syncthreads();
+      for (int e = t; e < ES * ES; e += 256) {
+        const int i = e % ES, j = e / ES;
+        const double v = i <= j ? T[i + j * ELD] : T[j + i * ELD];
+        A[(size_t)pair_row(Ik, Jk, i) + (size_t)pair_row(Il, Jl, j) * lda] = v;
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int gi = pair_row(Ik, Jk, i0 + a), gj = pair_row(Il, Jl, j0 + b);
+          A[(size_t)gi + (size_t)gj * lda] = c[a][b];
+          A[(size_t)gj + (size_t)gi * lda] = c[a][b];
+        }
+    }
+    return;
+  }
+  // B rows of pair k, 64-column chunk ch
+  bid -= ntiles;
+  const int nch = (m + ES - 1) / ES;
+  const int k = bid / nch, ch = bid % nch;
+  if (k >= np) return;
+  int Ik, Jk;
+  circle_pair(nb, round, k, &Ik, &Jk);
+  const double* Rkg = Rbuf + (size_t)k * ES * ES;
+  for (int e = t; e < ES * ES; e += 256) {
+    const int i = e % ES, j = e / ES, col = ch * ES + j;
+    T[i + j * ELD] = col < m ? B[(size_t)pair_row(Ik, Jk, i) + (size_t)col * ldb] : 0.0;
+    Rk[i + j * ELD] = Rkg[e];
+  }
+  __syncthreads();
+  double c[4][4];
+  gemm64<true>(Rk, T, c);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int col = ch * ES + j0 + b;
+      if (col < m) B[(size_t)pair_row(Ik, Jk, i0 + a) + (size_t)col * ldb] = c[a][b];
+    }
+}
+
+__global__ void eig_pad_kernel(const double* __restrict__ A, size_t lda, int n,
+                               double* __restrict__ W, int n2) {
+  const size_t tot = (size_t)n2 * n2;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e % n2), j = (int)(e / n2);
+    W[e] = (i < n && j < n) ? A[(size_t)i + (size_t)j * lda] : 0.0;
+  }
+}
+
+__global__ void eig_diag_kernel(const double* __restrict__ W, int n2, int n, double* __restrict__ lam) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    lam[i] = W[(size_t)i + (size_t)i * n2];
+}
+
+}  // namespace
+
+// lambda (n, device) = eigenvalues of the symmetric A (n x n, ld lda; read only), and
+// B (n x m, ld ldb) <- P^T B with A = P diag(lambda) P^T.  Eigenvalues in no particular order,
+// B's rows in the same order.  *sweeps: outer sweeps used.  Returns GPR_E_HIP (with a message)
+// if the iteration does not converge within GPR_EIG_MAX_SWEEPS (default 60).
+int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                  double* dlam, int* sweeps_out) {
+  if (n <= 0) return 0;
+  const int n2 = (n + ES - 1) / ES * ES;
+  const int nb = n2 / EB, np = nb / 2;
+  const int ntiles = np * (np + 1) / 2;
+  // workspace: W (n2 x n2), Bp (n2 x m), R (np x 64 x 64), rotation counter
+  const size_t need = (size_t)n2 * n2 + (size_t)n2 * std::max(m, 1) + (size_t)np * ES * ES + 1;
+  GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
+  double* W = ctx->deig;
+  double* Bp = W + (size_t)n2 * n2;
+  double* Rb = Bp + (size_t)n2 * std::max(m, 1);
+  int* rot = reinterpret_cast<int*>(Rb + (size_t)np * ES * ES);
+  hipStream_t s = ctx->stream;
+  eig_pad_kernel<<<1024, 256, 0, s>>>(dA, (size_t)lda, n, W, n2);
+  LAUNCH_CHECK(ctx);
+  if (m > 0) {
+    HIP_TRY(ctx, hipMemset2DAsync(Bp, (size_t)n2 * sizeof(double), 0, (size_t)n2 * sizeof(double), m, s));
+    HIP_TRY(ctx, hipMemcpy2DAsync(Bp, (size_t)n2 * sizeof(double), dB, (size_t)ldb * sizeof(double),
+                                  (size_t)n * sizeof(double), m, hipMemcpyDeviceToDevice, s));
+  }
+  static const int max_sweeps = getenv("GPR_EIG_MAX_SWEEPS") ? atoi(getenv("GPR_EIG_MAX_SWEEPS")) : 60;
+  static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 8;
+  const int nch = m > 0 ? (m + ES - 1) / ES : 0;
+  int sweep = 0, hrot = 1;
+  TimerScope ts(ctx, TC_OTHER, 0.0);
+  for (; sweep < max_sweeps && hrot; ++sweep) {
+    HIP_TRY(ctx, hipMemsetAsync(rot, 0, sizeof(int), s));
+    for (int r = 0; r < nb - 1; ++r) {
+      eig_subproblem_kernel<<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner);
+      eig_transform_kernel<<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
+                                                                (size_t)n2, m, ntiles);
+    }
+    LAUNCH_CHECK(ctx);
+    HIP_TRY(ctx, hipMemcpyAsync(&hrot, rot, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+  }
+  if (sweeps_out) *sweeps_out = sweep;
+  if (hrot) return set_err(ctx, GPR_E_HIP, "block Jacobi eigensolver: not converged after %d sweeps", sweep);
+  eig_diag_kernel<<<(n + 255) / 256, 256, 0, s>>>(W, n2, n, dlam);
+  LAUNCH_CHECK(ctx);
+  if (m > 0)
+    HIP_TRY(ctx, hipMemcpy2DAsync(dB, (size_t)ldb * sizeof(double), Bp, (size_t)n2 * sizeof(double),
+                                  (size_t)n * sizeof(double), m, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+extern "C" int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m,
+                              int ldb, double* dlam, int* sweeps) {
+  if (!ctx) return GPR_E_ARG;
+  if (n < 0 || m < 0 || lda < std::max(n, 1) || (m > 0 && ldb < std::max(n, 1)) ||
+      (n > 0 && (!dA || !dlam)) || (m > 0 && n > 0 && !dB))
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  return sym_eig_apply(ctx, dA, n, lda, dB, m, ldb, dlam, sweeps);
+}

@@ -171,6 +171,7 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   if (const char* e = getenv("GPR_PANEL")) ctx->panel_mode = atoi(e);
   if (const char* e = getenv("GPR_DAG")) ctx->dag_mode = atoi(e);
   if (const char* e = getenv("GPR_KBUILD_UPPER")) ctx->kbuild_upper = atoi(e);
+  if (const char* e = getenv("GPR_KBUILD_FULLCOLS")) ctx->kbuild_full_cols_nse = atoi(e);
   if (const char* e = getenv("GPR_DAG_NMIN")) ctx->dag_nmin = atoi(e);
   if (const char* e = getenv("GPR_DAG_NMAX")) ctx->dag_nmax = atoi(e);
   if (const char* e = getenv("GPR_DAG_TAIL")) ctx->dag_tail = atoi(e);
@@ -268,6 +269,7 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dgB) hipFree(ctx->dgB);
   if (ctx->dgc) hipFree(ctx->dgc);
   if (ctx->kup_items) hipFree(ctx->kup_items);
+  if (ctx->deig) hipFree(ctx->deig);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
   return 0;

@@ -777,7 +777,36 @@ __global__ __launch_bounds__(256) void quad_diag_update_kernel(const double* __r
 // (nothing done) when rocSOLVER cannot be loaded.
 static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k2, int n,
                              const double* dy, int ny, int ldy, const double* noise, double* Iout,
-                             double* var) {
+                             double* var, bool rocsolver) {
+  if (!rocsolver) {
+    // the hand-written block-Jacobi eigensolver (eigen.hip): lambda and T = P^T [Y | k1]
+    // directly, P never formed
+    const size_t nb = (size_t)n * (ny + 1);
+    GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, nb + (size_t)n + 3 * (size_t)ny));
+    double* T = ctx->dbig;
+    double* lam = T + nb;
+    double* dnoise = lam + n;
+    double* out = dnoise + ny;
+    HIP_TRY(ctx, hipMemcpy2DAsync(T, sizeof(double) * n, dy, sizeof(double) * ldy,
+                                  sizeof(double) * n, ny, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(T + (size_t)ny * n, k1, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise, sizeof(double) * ny, hipMemcpyHostToDevice,
+                                ctx->stream));
+    GPR_TRY(sym_eig_apply(ctx, K, n, n, T, ny + 1, n, lam, nullptr));
+    quad_diag_update_kernel<<<ny, 256, 0, ctx->stream>>>(T, n, ny, lam, dnoise, k2, out);
+    LAUNCH_CHECK(ctx);
+    std::vector<double> h(2 * (size_t)ny);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), out, sizeof(double) * 2 * ny, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int j = 0; j < ny; ++j) {
+      Iout[j] = h[2 * j];
+      var[j] = h[2 * j + 1];
+    }
+    return 0;
+  }
+  // GPR_QUAD_EIGEN=2: rocSOLVER dsyevd (a timing comparator for the hand-written solver)
   if (!load_rocsolver()) return 1;
   if (!ctx->rb_handle) {
     rocblas_handle hb = nullptr;
@@ -855,11 +884,14 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   double k2 = 0.0;
   GPR_TRY(gpr_antideriv_se(ctx, d, hp, dX, n, a, b, k1, &k2));
   // the reference's path: K = P diag(lambda) P^T once (LAPACK.syevr!, :75), then per column
-  // j only diagonal updates (inverse_diagonal_update!, :81-104).  GPR_QUAD_EIGEN=0, or no
-  // loadable rocSOLVER: K + noise_j I factored per column (PD shifts only)
+  // j only diagonal updates (inverse_diagonal_update!, :81-104) -- by the hand-written block-
+  // Jacobi eigensolver.  GPR_QUAD_EIGEN=0: K + noise_j I factored per column (PD shifts only);
+  // =2: rocSOLVER's dsyevd for the decomposition (timing comparator; falls back to the
+  // per-column factorisations when it cannot be loaded)
   const char* qe = getenv("GPR_QUAD_EIGEN");
-  if (!qe || atoi(qe) != 0) {
-    const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var);
+  const int qmode = qe ? atoi(qe) : 1;
+  if (qmode != 0) {
+    const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode == 2);
     if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
   }
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);

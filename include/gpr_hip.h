@@ -80,7 +80,9 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
 /* Per-kernel-class timing with HIP events on the context stream (bench instrumentation).
  * class: 0 K-assembly, 1 POTRF trailing update (SYRK), 2 POTRF panel (diag+TRSM),
  *        3 TRSM trailing GEMM, 4 other (call-site classes), 5 every launch of the
- *        pipelined MFMA GEMM kernel (kernel-level, overlaps 1-4).
+ *        pipelined MFMA GEMM kernel (kernel-level, overlaps 1-4), 6 tile-DAG factorisation
+ *        launches (with any right-hand sides they solve), 7 solve-only tile-DAG launches
+ *        (U^{-T} B from a finished factor: C5's variance rows, POTRI's Z).
  *        Returns accumulated ms, launch count, flops (bytes for class 0). */
 int gpr_timing_enable(gpr_ctx_t ctx, int on);
 int gpr_timing_get(gpr_ctx_t ctx, int cls, double* ms, long long* launches, double* flops);
@@ -237,17 +239,27 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
 /* integrate(md, hp, a, b; sample_noise = noise::Vector) (src/integrate.jl:71-100,149-162):
  * per column j of y (ny columns, noise[j] host), Iout[j] = k1' (K + noise_j I)^{-1} y_j and
  * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  As the reference: K = P Lambda P' once (the
- * reference's LAPACK syevr; here rocSOLVER dsyevd, dlopen'd -- the process's librocsolver.so.0
- * if loaded, else the system's), T = P' [y | k1] on the MFMA GEMM, then Iout[j] = sum_i
- * T_ij (P'k1)_i / (lambda_i + noise_j) and var[j] = k2 - sum_i (P'k1)_i^2 / (lambda_i +
- * noise_j): any shift, no factorisation, never info > 0 (an indefinite K + noise_j I gives
- * the reference's indefinite solve).  Without a loadable rocSOLVER, or with GPR_QUAD_EIGEN=0,
- * each K + noise_j I is factored by the MFMA POTRF instead (same quantities for positive
- * definite shifts; returns info > 0 -- PosDefException -- for the others). */
+ * reference's LAPACK syevr; here the hand-written block-Jacobi eigensolver of gpr_syev_apply,
+ * which never forms P: T = P' [y | k1] is carried through the rotations), then Iout[j] =
+ * sum_i T_ij (P'k1)_i / (lambda_i + noise_j) and var[j] = k2 - sum_i (P'k1)_i^2 / (lambda_i +
+ * noise_j): any shift, no factorisation, never info > 0 (an indefinite K + noise_j I gives the
+ * reference's indefinite solve).  GPR_QUAD_EIGEN=0: each K + noise_j I factored by the MFMA
+ * POTRF instead (positive definite shifts only; info > 0 -- PosDefException -- for the
+ * others); GPR_QUAD_EIGEN=2: rocSOLVER dsyevd (dlopen'd) for the decomposition -- a timing
+ * comparator, not the product path. */
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                         const double* dX, int n, const double* dy, int ny, int ldy,
                         const double* a, const double* b, const double* noise, double eps,
                         double* Iout, double* var);
+
+/* The symmetric eigendecomposition behind the sample_noise quadrature (LAPACK.syevr! at
+ * src/integrate.jl:75), applied instead of returned: A (n x n, ld lda, device, read only,
+ * symmetric) = P diag(lam) P'; on return dlam[n] (device) holds the eigenvalues -- in no
+ * particular order -- and dB (n x m, ld ldb, device) holds P' B, its rows in the order of
+ * dlam.  Two-sided block Jacobi (32-wide blocks, parallel ordering), FP64; *sweeps (may be
+ * NULL) = sweeps used.  GPR_E_HIP if it does not converge (GPR_EIG_MAX_SWEEPS, default 60). */
+int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                   double* dlam, int* sweeps);
 
 /* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
 /* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).

@@ -1,0 +1,118 @@
+"""The hand-written symmetric eigensolver (csrc/eigen.hip, block Jacobi) behind the
+sample_noise quadrature -- the reference's LAPACK.syevr! (src/integrate.jl:71-80), whose
+consumer (inverse_diagonal_update!, :81-104) only ever needs lambda and P^T B.
+
+gpr_syev_apply returns lambda and P^T B, never P; the checks are therefore on what is
+basis-independent:
+  * eigenvalues vs numpy.linalg.eigvalsh (sorted), |diff| <= 1e-13 ||A||_2 (backward stable)
+  * column norms of B preserved: ||P^T b|| = ||b|| (P orthogonal), rtol 1e-13
+  * the quantity the quadrature uses: (P^T B)^T diag(1/(lambda + s)) (P^T B) =
+    B^T (A + s I)^{-1} B, relative 1e-10 x cond(A + s I) for several shifts s (negative ones
+    included: the reference's eigen path takes any shift)
+on random symmetric matrices (ragged sizes, 1 to 1100) and on the reference's own SE kernel
+matrices (ill-conditioned, clustered spectra).  The oracle here is numpy's LAPACK.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import gpr_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = pytest.importorskip("gpr_amd")
+
+
+def _syev(ctx, A, B):
+    n = A.shape[0]
+    m = B.shape[1]
+    dA, dB = ctx.colmajor(A), ctx.colmajor(B)
+    lam = ctx.empty(max(n, 1))
+    sw = ctypes.c_int(-1)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rc = G._lib.lib.gpr_syev_apply(ctx.h, P(dA), n, max(n, 1), P(dB), m, max(n, 1), P(lam),
+                                   ctypes.byref(sw))
+    assert rc == 0, G._lib.lib.gpr_last_error(ctx.h)
+    return ctx.host(lam)[:n], ctx.host(dB), sw.value
+
+
+def _check(A, lam, C, B, shifts):
+    n = A.shape[0]
+    nrm = np.linalg.norm(A, 2)
+    ref = np.linalg.eigvalsh(A)
+    assert np.max(np.abs(np.sort(lam) - ref)) <= 1e-13 * max(nrm, 1e-300) + 1e-300
+    np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-13)
+    for s in shifts:
+        M = A + s * np.eye(n)
+        want = B.T @ np.linalg.solve(M, B)
+        got = C.T @ (C / (lam + s)[:, None])
+        ev = np.abs(ref + s)
+        cond = ev.max() / ev.min()
+        np.testing.assert_allclose(got, want, rtol=1e-10 * cond, atol=1e-10 * cond * np.abs(want).max())
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 31, 64, 65, 100, 129, 300, 511, 1100])
+def test_syev_random_symmetric(n):
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    B = rng.standard_normal((n, 3))
+    ctx = G.Context(0)
+    lam, C, sweeps = _syev(ctx, A, B)
+    assert 0 < sweeps < 60
+    ref = np.linalg.eigvalsh(A)
+    gap = np.min(np.abs(ref))
+    _check(A, lam, C, B, [s for s in (0.0, 0.5, -0.7) if np.min(np.abs(ref + s)) > 1e-3 * max(gap, 1e-3)])
+
+
+@pytest.mark.parametrize("kinds,dim,n,length", [([O.SE], 2, 150, 2.0), ([O.SE, O.WN], 3, 300, 2.0),
+                                               ([O.SE], 4, 1100, 2.0), ([O.SE], 1, 100, 1.0)])
+def test_syev_se_kernel_matrices(kinds, dim, n, length):
+    """The reference's matrices: K of SquaredExp (+ WhiteNoise) on U[0,1) points -- PSD, a
+    spectrum decaying to the 1e-8 jitter plateau (clusters of nearly equal eigenvalues)."""
+    rng = np.random.default_rng(dim * n)
+    x = rng.random((dim, n))
+    hp = O.default_hp(kinds, dim, length=length, noise=0.05)
+    K = O.kernel(kinds, hp, x)
+    B = np.c_[rng.random((n, 2)), O.antideriv_se(x, hp, np.zeros(dim), np.ones(dim))]
+    ctx = G.Context(0)
+    lam, C, _ = _syev(ctx, K, B)
+    lmin = np.linalg.eigvalsh(K).min()
+    _check(K, lam, C, B, [1e-3, 1e-5, -0.5 * lmin if lmin > 1e-6 else 1e-2])
+
+
+def test_syev_diagonal_and_zero():
+    """Already diagonal (no rotation at all: exact), the zero matrix, and a 2 x 2 block."""
+    ctx = G.Context(0)
+    d = np.array([3.0, -1.0, 2.0, 0.0, 7.5])
+    B = np.arange(10.0).reshape(5, 2)
+    lam, C, sweeps = _syev(ctx, np.diag(d), B)
+    assert sweeps == 1 and np.array_equal(lam, d) and np.array_equal(C, B)
+    lam, C, _ = _syev(ctx, np.zeros((70, 70)), np.ones((70, 1)))
+    assert np.array_equal(lam, np.zeros(70)) and np.array_equal(C, np.ones((70, 1)))
+    A = np.array([[2.0, 1.0], [1.0, 2.0]])
+    lam, C, _ = _syev(ctx, A, np.eye(2))
+    np.testing.assert_allclose(np.sort(lam), [1.0, 3.0], rtol=1e-15)
+    np.testing.assert_allclose(np.abs(C), np.sqrt(0.5), rtol=1e-15)
+
+
+def test_integrate_noise_native_vs_rocsolver_comparator(monkeypatch):
+    """The product path (hand-written eigensolver) against rocSOLVER's dsyevd as a comparator
+    (GPR_QUAD_EIGEN=2, timing/cross-check only) and against the oracle's eigen path."""
+    dim, n, ne = 3, 600, 6
+    kinds = [O.SE, O.WN]
+    rng = np.random.default_rng(9)
+    x = rng.random((dim, n))
+    Y = rng.random((n, ne))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    noise = np.r_[1e-3 * (1.0 + rng.random(ne - 1)), -1e-3]
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I, Io, rtol=1e-8)
+    np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
+    monkeypatch.setenv("GPR_QUAD_EIGEN", "2")
+    I2, v2 = G.integrate(md, a, b, sample_noise=noise)
+    np.testing.assert_allclose(I2, I, rtol=1e-8)
+    np.testing.assert_allclose(v2, v, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))

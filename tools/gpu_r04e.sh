@@ -1,0 +1,8 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_eigen.py tests/test_integrate.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/tests_r04e.log 2>&1
+echo "tests rc=$?"; grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/tests_r04e.log | tail -40
+rm -f gpurun_out/kb_r04e.txt
+for k in SE SE+SE+WN; do GPR_KBUILD_FULLCOLS=2 KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench | grep -E "sym|upper" | sed 's/^/fullcols2 /' >> gpurun_out/kb_r04e.txt 2>&1; GPR_KBUILD_FULLCOLS=2 KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_nostore | grep -E "sym" | sed 's/^/nostore fullcols2 /' >> gpurun_out/kb_r04e.txt 2>&1; done
+cat gpurun_out/kb_r04e.txt
+timeout -k 10 200 python bench_split.py --var-rows 1024 --steps 1 --warmup 1 > gpurun_out/bench_split_full_r04e.json 2> gpurun_out/bench_split_full_r04e.err; echo "split rc=$?"; cat gpurun_out/bench_split_full_r04e.json

@@ -128,6 +128,54 @@ __global__ void store16nt_kernel(double* p, size_t n2) {
     __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(p) + i);
 }
 
+// ---- write patterns of an upper-only build (column c: rows [0, min(N, 128 (c/128 + 1)))) ----
+__host__ __device__ inline int up_rows(int c, int N) { return min(N, 128 * (c / 128 + 1)); }
+// (a) the kmat_symu_kernel shape: one wave per (32-column strip, 256-row segment), 8-B stores,
+//     one instruction = 4 columns x 128 contiguous bytes
+__global__ void st_up_kup(double* K, int N, size_t ld, const int* items, int nitems) {
+  const int lane = threadIdx.x & 63;
+  const int voff = (lane & 15) + (lane >> 4) * (int)ld;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nitems; t += gridDim.x * 4) {
+    const int code = items[t];
+    const int j0 = (code >> 16) * 32, r0 = (code & 0xffff) * 256;
+    const int r1 = min(r0 + 256, up_rows(j0, N));
+    for (int i0 = r0; i0 < r1; i0 += 32)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            __builtin_nontemporal_store(1.0, K + (size_t)(i0 + 16 * rb) + (size_t)(j0 + 16 * cb + 4 * q) * ld + voff);
+  }
+}
+// (b) the same items, 16-B stores: one instruction = 128 rows (1 KB) of one column
+__global__ void st_up_col16(double* K, int N, size_t ld, const int* items, int nitems) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nitems; t += gridDim.x * 4) {
+    const int code = items[t];
+    const int j0 = (code >> 16) * 32, r0 = (code & 0xffff) * 256;
+    const int r1 = min(r0 + 256, up_rows(j0, N));
+    for (int i0 = r0; i0 < r1; i0 += 32)     // (the kernel's 32-row units: 32 columns x 32 rows =
+#pragma unroll                              //  16 half-instructions; here 8 x 2 columns)
+      for (int c = 0; c < 32; c += 4) {
+        const int cc = c + (lane >> 4);
+        __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(K + (size_t)i0 + 2 * (lane & 15) + (size_t)(j0 + cc) * ld));
+      }
+  }
+}
+// (c) whole 1-KB column chunks in column order (the flat ideal of an upper-only write)
+__global__ void st_up_flat(double* K, int N, size_t ld, const long long* chunk0, int nch) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nch; t += gridDim.x * 4) {
+    const long long code = chunk0[t];
+    const int c = (int)(code >> 20), r = (int)(code & 0xfffff);
+    __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(K + (size_t)r + 2 * lane + (size_t)c * ld));
+  }
+}
+
 int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 32768;
   const int d = argc > 2 ? atoi(argv[2]) : 8;
@@ -250,6 +298,40 @@ int main(int argc, char** argv) {
       timeit([&] { storepair_kernel<<<ntp, 256, 0, s>>>(K, N, ntp, ld); }, "storepair 1 tile/WG");
       timeit([&] { store16_kernel<<<(unsigned)(bytes / 16 / 256 / 16), 256, 0, s>>>(K, bytes / 16); }, "store16 16/thread grid-stride");
     }
+  }
+  if (getenv("KB_UPPAT")) {  // upper-only write patterns, 4.31 GB at N = 32768
+    std::vector<int> items;
+    std::vector<long long> chunks;
+    for (int bj = 0; bj * 32 < N; ++bj)
+      for (int sg = 0; sg * 256 < up_rows(bj * 32, N); ++sg) items.push_back((bj << 16) | sg);
+    for (int c = 0; c < N; ++c)
+      for (int r = 0; r < up_rows(c, N); r += 128) chunks.push_back(((long long)c << 20) | r);
+    int* ditems; long long* dch;
+    hipMalloc(&ditems, items.size() * sizeof(int));
+    hipMalloc(&dch, chunks.size() * sizeof(long long));
+    hipMemcpy(ditems, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice);
+    hipMemcpy(dch, chunks.data(), chunks.size() * sizeof(long long), hipMemcpyHostToDevice);
+    const double bytes = 8.0 * 128.0 * chunks.size();
+    auto t2 = [&](auto launch, const char* what) {
+      float best = 1e30f;
+      for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(e0, s); launch(); hipEventRecord(e1, s); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best = ms < best ? ms : best;
+      }
+      printf("uppat %-26s %.3f ms  %.0f GB/s (%.1f%%)\n", what, best, bytes / best / 1e6, bytes / best / 1e6 / 80.0);
+    };
+    for (int g : {1024, 2048, 4096}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "kup8 grid %d", g);
+      t2([&] { st_up_kup<<<g, 256, 0, s>>>(K, N, ld, ditems, (int)items.size()); }, nm);
+      snprintf(nm, sizeof nm, "col16 grid %d", g);
+      t2([&] { st_up_col16<<<g, 256, 0, s>>>(K, N, ld, ditems, (int)items.size()); }, nm);
+      snprintf(nm, sizeof nm, "flat grid %d", g);
+      t2([&] { st_up_flat<<<g, 256, 0, s>>>(K, N, ld, dch, (int)chunks.size()); }, nm);
+    }
+    t2([&] { st_up_flat<<<(unsigned)(chunks.size() + 3) / 4, 256, 0, s>>>(K, N, ld, dch, (int)chunks.size()); }, "flat 1 chunk/wave");
+    return 0;
   }
   struct Cfg { const char* name; std::vector<int> kinds; };
   std::vector<Cfg> cfgs = {{"SE", {GPR_SE}}, {"SE+WN", {GPR_SE, GPR_WN}}, {"SE+SE+WN", {GPR_SE, GPR_SE, GPR_WN}}};

@@ -805,57 +805,69 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
                                          double* __restrict__ K, size_t ldk, int i0, int j0,
                                          int r1, int n, int voff) {
   const int lane = threadIdx.x & 63;
-  // block by block: its parts' MFMAs, then its 4 x NSE exponentials, then its 4 stores.  The
-  // empty asm statements pin each finished value where it is made: without them the compiler
+  // block by block, software-pipelined: the next block's MFMAs are issued before this block's
+  // exponentials (their 64-cycle results are not waited for), then its 4 x NSE exponentials --
+  // four independent chains per part, pinned as a group -- then its 4 stores.  The empty asm
+  // statements pin each group's finished values where they are made: without them the compiler
   // sank the second half of every exponential down to the stores and kept all 16 in flight
-  // (200+ registers, one wave per SIMD)
+  // (200+ registers, one wave per SIMD); pinned one by one, the chains ran serially (each
+  // exponential waited for its own table read)
+  auto mfma_block = [&](int blk, gd4 (&acc)[NSE]) {
+    const int rb = blk >> 1, cb = blk & 1;
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+    for (int p = 0; p < NSE; ++p) {
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      gd4 acc[NSE];
+      for (int q = 0; q < 4; ++q)
+        acc[p][q] = rn[p][rb] + cn[KU_W * p + 16 * cb + (lane >> 4) + 4 * q];
 #pragma unroll
-      for (int p = 0; p < NSE; ++p) {
+      for (int s = 0; s < S; ++s)
+        acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[p][cb][s], ra[p][rb][s], acc[p], 0, 0, 0);
+    }
+  };
+  gd4 acc[NSE], accn[NSE];
+  mfma_block(0, acc);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          acc[p][q] = rn[p][rb] + cn[KU_W * p + 16 * cb + (lane >> 4) + 4 * q];
+  for (int blk = 0; blk < 4; ++blk) {
+    const int rb = blk >> 1, cb = blk & 1;
+    if (blk < 3) mfma_block(blk + 1, accn);
+    double v[4];
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[p][cb][s], ra[p][rb][s], acc[p], 0, 0, 0);
-      }
-      double v[4];
-#pragma unroll
-      for (int p = 0; p < NSE; ++p) {
-        const double* ts = tabs + 256 * p;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          double x = acc[p][q];  // -D
-          bool on = false;
-          if (DIAG) {
-            on = rb == cb && (lane & 15) == (lane >> 4) + 4 * q;
-            if (on) x = 0.0;
-          }
-          double e = CLAMP ? kexp_s2(-x, ts) : kexp_s2_nc(-x, ts);
-          if (DIAG && on) e += kp.eps;
-          v[q] = p == 0 ? e : v[q] + e;
-          asm volatile("" : "+v"(v[q]));
-        }
-      }
+    for (int p = 0; p < NSE; ++p) {
+      const double* ts = tabs + 256 * p;
+      double e[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        double val = v[q];
-        if (DIAG && kp.has_noise && rb == cb && (lane & 15) == (lane >> 4) + 4 * q) val += kp.noise2;
-        // uniform base (SGPR) + the lane's 32-bit offset: rows 16 rb + (lane & 15), columns
-        // 16 cb + 4 q + (lane >> 4) of the unit
-        double* base = K + (size_t)(i0 + 16 * rb) + (size_t)(j0 + 16 * cb + 4 * q) * ldk;
-#ifdef GPR_KBUILD_NOSTORE  // diagnostics (tools/kbuild_bench_nostore): compute-only timing
-        if (!(val == val)) base[voff] = val;
-#else
-        if (!EDGE || (i0 + 16 * rb + (lane & 15) < r1 && j0 + 16 * cb + 4 * q + (lane >> 4) < n))
-          __builtin_nontemporal_store(val, base + voff);
-#endif
+        double x = acc[p][q];  // -D
+        bool on = false;
+        if (DIAG) {
+          on = rb == cb && (lane & 15) == (lane >> 4) + 4 * q;
+          if (on) x = 0.0;
+        }
+        e[q] = CLAMP ? kexp_s2(-x, ts) : kexp_s2_nc(-x, ts);
+        if (DIAG && on) e[q] += kp.eps;
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = p == 0 ? e[q] : v[q] + e[q];
+      asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double val = v[q];
+      if (DIAG && kp.has_noise && rb == cb && (lane & 15) == (lane >> 4) + 4 * q) val += kp.noise2;
+      // uniform base (SGPR) + the lane's 32-bit offset: rows 16 rb + (lane & 15), columns
+      // 16 cb + 4 q + (lane >> 4) of the unit
+      double* base = K + (size_t)(i0 + 16 * rb) + (size_t)(j0 + 16 * cb + 4 * q) * ldk;
+#ifdef GPR_KBUILD_NOSTORE  // diagnostics (tools/kbuild_bench_nostore): compute-only timing
+      if (!(val == val)) base[voff] = val;
+#else
+      if (!EDGE || (i0 + 16 * rb + (lane & 15) < r1 && j0 + 16 * cb + 4 * q + (lane >> 4) < n))
+        __builtin_nontemporal_store(val, base + voff);
+#endif
+    }
+    if (blk < 3)
+#pragma unroll
+      for (int p = 0; p < NSE; ++p) acc[p] = accn[p];
+  }
 }
 
 template <int S, int NSE>

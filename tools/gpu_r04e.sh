@@ -6,3 +6,6 @@ rm -f gpurun_out/kb_r04e.txt
 for k in SE SE+SE+WN; do GPR_KBUILD_FULLCOLS=2 KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench | grep -E "sym|upper" | sed 's/^/fullcols2 /' >> gpurun_out/kb_r04e.txt 2>&1; GPR_KBUILD_FULLCOLS=2 KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_nostore | grep -E "sym" | sed 's/^/nostore fullcols2 /' >> gpurun_out/kb_r04e.txt 2>&1; done
 cat gpurun_out/kb_r04e.txt
 timeout -k 10 200 python bench_split.py --var-rows 1024 --steps 1 --warmup 1 > gpurun_out/bench_split_full_r04e.json 2> gpurun_out/bench_split_full_r04e.err; echo "split rc=$?"; cat gpurun_out/bench_split_full_r04e.json
+timeout -k 10 600 bash tools/gpu_clock_stream.sh; echo "clock rc=$?"; cat gpurun_out/clock_stream/probe.txt
+timeout -k 10 60 ./tools/probe/mfma_valu_overlap > gpurun_out/mfma_valu_overlap.txt 2>&1; echo "overlap rc=$?"; cat gpurun_out/mfma_valu_overlap.txt
+for r in 1 2; do for k in SE SE+SE+WN; do KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_v1 | grep -E "upper" | sed "s/^/v1 /"; KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench | grep -E "upper" | sed "s/^/v2 /"; KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_nostore | grep -E "upper" | sed "s/^/v2 nostore /"; KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_v2m2 | grep -E "upper" | sed "s/^/v2m2 /"; done; done > gpurun_out/kb_v1v2.txt 2>&1; cat gpurun_out/kb_v1v2.txt

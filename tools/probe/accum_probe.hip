@@ -51,7 +51,9 @@ __global__ __launch_bounds__(NW * 64, 1) void accum_kernel(const double* __restr
   // of tasks), Q distinct per workgroup (every task its own column panel).  P spans TMR
   // consecutive panels, so it starts at most at panel ncolblk - TMR - 1.
   const int np_ = ncolblk - TMR - 1;
-  const int pp = mode ? (b / 32) % np_ : 0, qp = mode ? TMR + (b % np_) : TMR;
+  // mode 2 (L2-resident): mode 0's operands, K wrapped at 1024 rows (64 stages): 2 MB of
+  // operands per launch, held in every XCD's 4-MB L2 -- the same MFMA work with no HBM stream
+  const int pp = mode == 1 ? (b / 32) % np_ : 0, qp = mode == 1 ? TMR + (b % np_) : TMR;
   const double* P = M + (size_t)pp * DT * ld;
   const double* Q = M + (size_t)qp * DT * ld;
   d4v acc[4][RB];
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(NW * 64, 1) void accum_kernel(const double* __restr
   }
   auto issue = [&](int s) {
     double* base = lds + (s % NSTG) * DSTAGE;
-    const size_t ko = (size_t)min(s, nst - 1) * DTK;
+    const size_t ko = (size_t)(mode == 2 ? min(s, nst - 1) & 63 : min(s, nst - 1)) * DTK;
 #pragma unroll
     for (int r = 0; r < NDP; ++r)
       __builtin_amdgcn_global_load_lds(srcP[r] + ko, base + (NW * r + w) * 128, 16, 0, 0);
@@ -360,7 +362,8 @@ void run(const double* M, size_t ld, int ncolblk, int K, int reps, int mode, dou
   const double flops = 2.0 * DT * TMR * DT * (double)nst * DTK * cus * reps;
   const double bytes = 8.0 * (DT * TMR + DT) * (double)nst * DTK * cus * reps;
   printf("%s tile %3dx128, %d waves, %d stages (%3zu KB), %s fragments: %.2f TFLOP/s = %.4f per CU, "
-         "%.1f flop/B, operand stream %.2f TB/s (%.3f ms per launch)\n", mode ? "dag-like" : "hot     ",
+         "%.1f flop/B, operand stream %.2f TB/s (%.3f ms per launch)\n",
+         mode == 1 ? "dag-like" : mode == 2 ? "L2-held " : "hot     ",
          DT * TMR, NW, NSTG, lds / 1024, DBUF ? "2-set" : "1-set", flops / ms / 1e9,
          flops / ms / 1e9 / cus, flops / bytes, bytes / ms / 1e9, ms / reps);
 }

@@ -135,7 +135,10 @@ def parse():
     ap.add_argument("--no-split", action="store_true",
                     help="skip the C5 split-predict leg (extra key `split_predict`)")
     ap.add_argument("--split-steps", type=int, default=2)
-    ap.add_argument("--split-timeout", type=float, default=300.0,
+    ap.add_argument("--no-split-full", dest="split_full", action="store_false",
+                    help="skip the C5 leg's full-range variant (var_range = 1:ne, SURVEY 8d's "
+                         "throughput configuration: ~17 s per step on one GPU, 1 warm-up + 1 step)")
+    ap.add_argument("--split-timeout", type=float, default=420.0,
                     help="watchdog: end the process (exit 0, headline already printed) if the "
                          "C5 leg runs longer than this many seconds")
     # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices by
@@ -302,17 +305,17 @@ def split_leg(a, world, rank, local):
     flops = 2.0 * ne * ns * nq + float(nq) * ns * ns * vr
     coll = "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
 
-    def timed(fit):
-        step = lambda: split_predict_distributed(md, cm, var_range=(1, vr), fit=fit)  # noqa: E731
+    def timed(fit, rows=vr, steps=a.split_steps):
+        step = lambda: split_predict_distributed(md, cm, var_range=(1, rows), fit=fit)  # noqa: E731
         step()
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(a.split_steps):
+        for _ in range(steps):
             mu, var = step()
         torch.cuda.synchronize()
         dist.barrier()
-        dt = (time.perf_counter() - t0) / a.split_steps
+        dt = (time.perf_counter() - t0) / steps
         tt = torch.tensor([dt], dtype=torch.float64,
                           device=f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -330,6 +333,12 @@ def split_leg(a, world, rank, local):
         dt_r, ok_r = timed("replicate")
         out["replicate"] = {"value": ne * nq / dt_r, "ms_per_step": dt_r * 1e3,
                             "results_finite": ok_r}
+    if a.split_full:  # SURVEY 8d's throughput configuration: variance for every grid row
+        dt_f, ok_f = timed("broadcast", rows=ne, steps=1)
+        flops_f = 2.0 * ne * ns * nq + float(nq) * ns * ns * ne
+        out["full_var_range"] = {"value": ne * nq / dt_f, "ms_per_step": dt_f * 1e3, "steps": 1,
+                                 "var_rows": ne, "algorithmic_TFLOPs": flops_f / dt_f / 1e12,
+                                 "results_finite": ok_f}
     return out
 
 

@@ -52,12 +52,34 @@ __device__ __forceinline__ int pair_row(int I, int J, int i) {
   return i < EB ? EB * I + i : EB * J + (i - EB);
 }
 
+// thread t computes the 4 x 4 block rows 4 (t % 16).., columns 4 (t / 16).. of the 64 x 64
+// product C = TA ? X^T Y : X Y  (X, Y in LDS, row stride ELD)
+template <bool TA>
+__device__ __forceinline__ void gemm64(const double* X, const double* Y, double (&c)[4][4]) {
+  const int t = threadIdx.x, i0 = 4 * (t % 16), j0 = 4 * (t / 16);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) c[a][b] = 0.0;
+  for (int kk = 0; kk < ES; ++kk) {
+    double x[4], y[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) x[a] = TA ? X[kk + (i0 + a) * ELD] : X[(i0 + a) + kk * ELD];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) y[b] = Y[kk + (j0 + b) * ELD];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) c[a][b] = fma(x[a], y[b], c[a][b]);
+  }
+}
+
 // 1. per pair: diagonalise S = A[P, P] by parallel Jacobi in LDS, R = accumulated rotation
 __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __restrict__ A, size_t lda,
                                                             int nb, int round,
                                                             double* __restrict__ Rbuf,
                                                             int* __restrict__ rotations,
-                                                            int max_inner) {
+                                                            int max_inner, int reorth) {
   __shared__ double S[ES * ELD];
   __shared__ double R[ES * ELD];
   __shared__ double cs[ES / 2][2];
@@ -130,31 +152,35 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
     __syncthreads();  // (every thread has read rot_sweep before thread 0 resets it)
     if (rs == 0) break;
   }
-  double* Rk = Rbuf + (size_t)k * ES * ES;
-  for (int e = t; e < ES * ES; e += 256) Rk[e] = R[(e % ES) + (e / ES) * ELD];
-  if (t == 0 && rot_total) atomicAdd(rotations, rot_total);
-}
-
-// C (64 x 64, LDS stride ELD) = op(X)^T-or-not ... : thread t computes the 4 x 4 block
-// rows 4 (t % 16).., columns 4 (t / 16)..  of  C = TA ? X^T Y : X Y  (X, Y in LDS, stride ELD)
-template <bool TA>
-__device__ __forceinline__ void gemm64(const double* X, const double* Y, double (&c)[4][4]) {
-  const int t = threadIdx.x, i0 = 4 * (t % 16), j0 = 4 * (t / 16);
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) c[a][b] = 0.0;
-  for (int kk = 0; kk < ES; ++kk) {
-    double x[4], y[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) x[a] = TA ? X[kk + (i0 + a) * ELD] : X[(i0 + a) + kk * ELD];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) y[b] = Y[kk + (j0 + b) * ELD];
+  // R accumulated hundreds of rotations and drifted from orthogonality by ~sqrt(count) ulps;
+  // applied round after round, that drift (not the rotations' own rounding) set the
+  // eigenvalue error.  One Newton-Schulz step R <- R (3 I - R^T R) / 2 takes it to rounding
+  // level (quadratic: 1e-14 -> 1e-28) -- two 64^3 products in LDS, S's space holding R^T R.
+  if (reorth && rot_total) {
+    const int i0 = 4 * (t % 16), j0 = 4 * (t / 16);
+    double c[4][4];
+    gemm64<true>(R, R, c);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) c[a][b] = fma(x[a], y[b], c[a][b]);
+      for (int b = 0; b < 4; ++b) S[(i0 + a) + (j0 + b) * ELD] = c[a][b];
+    __syncthreads();
+    gemm64<false>(R, S, c);  // R (R^T R)
+    double r[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) r[a][b] = 1.5 * R[(i0 + a) + (j0 + b) * ELD] - 0.5 * c[a][b];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) R[(i0 + a) + (j0 + b) * ELD] = r[a][b];
+    __syncthreads();
   }
+  double* Rk = Rbuf + (size_t)k * ES * ES;
+  for (int e = t; e < ES * ES; e += 256) Rk[e] = R[(e % ES) + (e / ES) * ELD];
+  if (t == 0 && rot_total) atomicAdd(rotations, rot_total);
 }
 
 // 2. A[P_k, P_l] <- R_k^T A[P_k, P_l] R_l for every tile k <= l (mirrored into (l, k)), and
@@ -290,13 +316,14 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
   }
   static const int max_sweeps = getenv("GPR_EIG_MAX_SWEEPS") ? atoi(getenv("GPR_EIG_MAX_SWEEPS")) : 60;
   static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 8;
+  static const int reorth = getenv("GPR_EIG_REORTH") ? atoi(getenv("GPR_EIG_REORTH")) : 1;
   const int nch = m > 0 ? (m + ES - 1) / ES : 0;
   int sweep = 0, hrot = 1;
   TimerScope ts(ctx, TC_OTHER, 0.0);
   for (; sweep < max_sweeps && hrot; ++sweep) {
     HIP_TRY(ctx, hipMemsetAsync(rot, 0, sizeof(int), s));
     for (int r = 0; r < nb - 1; ++r) {
-      eig_subproblem_kernel<<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner);
+      eig_subproblem_kernel<<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
       eig_transform_kernel<<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
                                                                 (size_t)n2, m, ntiles);
     }

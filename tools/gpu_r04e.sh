@@ -9,3 +9,4 @@ timeout -k 10 200 python bench_split.py --var-rows 1024 --steps 1 --warmup 1 > g
 timeout -k 10 600 bash tools/gpu_clock_stream.sh; echo "clock rc=$?"; cat gpurun_out/clock_stream/probe.txt
 timeout -k 10 60 ./tools/probe/mfma_valu_overlap > gpurun_out/mfma_valu_overlap.txt 2>&1; echo "overlap rc=$?"; cat gpurun_out/mfma_valu_overlap.txt
 for r in 1 2; do for k in SE SE+SE+WN; do KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_v1 | grep -E "upper" | sed "s/^/v1 /"; KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench | grep -E "upper" | sed "s/^/v2 /"; KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_nostore | grep -E "upper" | sed "s/^/v2 nostore /"; KB_ONLY=$k timeout -k 10 60 ./tools/kbuild_bench_v2m2 | grep -E "upper" | sed "s/^/v2m2 /"; done; done > gpurun_out/kb_v1v2.txt 2>&1; cat gpurun_out/kb_v1v2.txt
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "fit_buffer or kernel_matrix or kernel_same or predict_vs_oracle" > gpurun_out/tests_r04e_kb.log 2>&1; echo "kb tests rc=$?"; tail -3 gpurun_out/tests_r04e_kb.log

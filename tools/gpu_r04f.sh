@@ -1,0 +1,6 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+for v in "GPR_EIG_REORTH=0" "GPR_EIG_REORTH=1" "GPR_EIG_REORTH=1 GPR_EIG_INNER=2" "GPR_EIG_REORTH=1 GPR_EIG_INNER=1"; do
+  echo "== $v"; env $v timeout -k 10 240 python tools/eig_probe.py 2>&1 | grep -v amdgpu.ids || exit 1
+done > gpurun_out/eig_probe_r04f.txt 2>&1
+echo "probe rc=$?"; cat gpurun_out/eig_probe_r04f.txt

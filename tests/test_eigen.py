@@ -4,7 +4,8 @@ consumer (inverse_diagonal_update!, :81-104) only ever needs lambda and P^T B.
 
 gpr_syev_apply returns lambda and P^T B, never P; the checks are therefore on what is
 basis-independent:
-  * eigenvalues vs numpy.linalg.eigvalsh (sorted), |diff| <= 1e-13 ||A||_2 (backward stable)
+  * eigenvalues vs numpy.linalg.eigvalsh (sorted), |diff| <= 4 n eps ||A||_2 (backward
+    stability's bound, which LAPACK's own answer shares)
   * column norms of B preserved: ||P^T b|| = ||b|| (P orthogonal), rtol 1e-13
   * the quantity the quadrature uses: (P^T B)^T diag(1/(lambda + s)) (P^T B) =
     B^T (A + s I)^{-1} B, relative 1e-10 x cond(A + s I) for several shifts s (negative ones
@@ -40,7 +41,8 @@ def _check(A, lam, C, B, shifts):
     n = A.shape[0]
     nrm = np.linalg.norm(A, 2)
     ref = np.linalg.eigvalsh(A)
-    assert np.max(np.abs(np.sort(lam) - ref)) <= 1e-13 * max(nrm, 1e-300) + 1e-300
+    eps = np.finfo(float).eps
+    assert np.max(np.abs(np.sort(lam) - ref)) <= 4 * n * eps * max(nrm, 1e-300) + 1e-300
     np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-13)
     for s in shifts:
         M = A + s * np.eye(n)

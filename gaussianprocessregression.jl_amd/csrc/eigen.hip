@@ -6,11 +6,13 @@
 // multiple of 64 with zero rows/columns, which stay decoupled) is split into 32-wide blocks;
 // a round pairs every block with another (the circle method: nb - 1 rounds per sweep meet
 // every pair once).  Per round:
-//   1. one workgroup per pair (I, J) runs up to two sweeps of scalar parallel Jacobi on its
-//      64 x 64 subproblem S = K[I u J, I u J] in LDS (32 disjoint rotations per step, 63 steps
-//      per sweep; GPR_EIG_INNER; more inner sweeps did not reduce the outer ones in the CPU
-//      emulation, tools/eig_emulate.py), re-orthogonalises the accumulated rotation R by one
-//      Newton-Schulz step and writes it (64 x 64);
+//   1. one workgroup per pair (I, J) runs one sweep of scalar parallel Jacobi on its 64 x 64
+//      subproblem S = K[I u J, I u J] in LDS (32 disjoint rotations per step, 63 steps;
+//      GPR_EIG_INNER sweeps: 1, 2 and 8 measured 111 / 183 / 177 ms at n = 1100 with 13 outer
+//      sweeps each, profiles/r04_eig_probe.txt), re-orthogonalises the accumulated rotation R
+//      by one Newton-Schulz step (without it R's drift set the eigenvalue error: 3-9 n eps
+//      |K|, orthogonality of P 300-15000 eps; with it 0.03-0.2 n eps |K| and 3-54 eps) and
+//      writes it (64 x 64);
 //   2. every 64 x 64 tile of K in pair coordinates becomes R_k^T K[P_k, P_l] R_l (computed for
 //      k <= l and mirrored, so K stays exactly symmetric) and the pair's rows of B become
 //      R_k^T B[P_k, :] -- all pairs' transforms at once, J^T K J with J = diag(R_k).
@@ -317,7 +319,7 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
                                   (size_t)n * sizeof(double), m, hipMemcpyDeviceToDevice, s));
   }
   static const int max_sweeps = getenv("GPR_EIG_MAX_SWEEPS") ? atoi(getenv("GPR_EIG_MAX_SWEEPS")) : 60;
-  static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 2;
+  static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 1;
   static const int reorth = getenv("GPR_EIG_REORTH") ? atoi(getenv("GPR_EIG_REORTH")) : 1;
   const int nch = m > 0 ? (m + ES - 1) / ES : 0;
   int sweep = 0, hrot = 1;

@@ -6,3 +6,4 @@ done > gpurun_out/eig_probe_r04f.txt 2>&1
 echo "probe rc=$?"; cat gpurun_out/eig_probe_r04f.txt
 timeout -k 10 500 python -u -m pytest tests/test_eigen.py tests/test_integrate.py -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/tests_r04f.log 2>&1
 echo "tests rc=$?"; grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/tests_r04f.log | tail -40
+KB_FULLPAT=1 timeout -k 10 120 ./tools/kbuild_bench > gpurun_out/kb_fullpat.txt 2>&1; echo "fullpat rc=$?"; grep fullpat gpurun_out/kb_fullpat.txt

@@ -176,6 +176,36 @@ __global__ void st_up_flat(double* K, int N, size_t ld, const long long* chunk0,
   }
 }
 
+// ---- write patterns of a FULL column build (every column c: rows [0, N)) -----------------
+// (d) one wave per (W-column strip, H-row segment), strip-major items, grid-stride over the
+//     items; each store instruction = one column's H rows as 16-B lanes when H = 128 (1 KB),
+//     or (kup8 shape) 4 columns x 128 B with 8-B lanes
+template <int WCOL, int H, bool K8>
+__global__ void st_full_items(double* K, int N, size_t ld, int nitems) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int nseg = N / H;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nitems; t += gridDim.x * 4) {
+    const int j0 = (t / nseg) * WCOL, r0 = (t % nseg) * H;
+    if (K8) {
+      const int voff = (lane & 15) + (lane >> 4) * (int)ld;
+      for (int i0 = r0; i0 < r0 + H; i0 += 32)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < WCOL / 16; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              __builtin_nontemporal_store(1.0, K + (size_t)(i0 + 16 * rb) + (size_t)(j0 + 16 * cb + 4 * q) * ld + voff);
+    } else {
+#pragma unroll 4
+      for (int c = 0; c < WCOL; ++c)
+        for (int i = 2 * lane; i < H; i += 128)
+          __builtin_nontemporal_store(d2{1.0, 2.0}, reinterpret_cast<d2*>(K + (size_t)r0 + i + (size_t)(j0 + c) * ld));
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 32768;
   const int d = argc > 2 ? atoi(argv[2]) : 8;
@@ -331,6 +361,34 @@ int main(int argc, char** argv) {
       t2([&] { st_up_flat<<<g, 256, 0, s>>>(K, N, ld, dch, (int)chunks.size()); }, nm);
     }
     t2([&] { st_up_flat<<<(unsigned)(chunks.size() + 3) / 4, 256, 0, s>>>(K, N, ld, dch, (int)chunks.size()); }, "flat 1 chunk/wave");
+    return 0;
+  }
+  if (getenv("KB_FULLPAT")) {  // full-matrix column-build write patterns, 8.59 GB
+    const double bytes = 8.0 * (double)N * N;
+    auto t3 = [&](auto launch, const char* what) {
+      float best = 1e30f;
+      for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(e0, s); launch(); hipEventRecord(e1, s); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        if (rep) best = ms < best ? ms : best;
+      }
+      printf("fullpat %-34s %.3f ms  %.0f GB/s (%.1f%%)\n", what, best, bytes / best / 1e6, bytes / best / 1e6 / 80.0);
+    };
+    t3([&] { store16flat_kernel<<<(unsigned)(bytes / 16 / 256), 256, 0, s>>>(K); }, "store16flat");
+    for (int g : {1024, 2048}) {
+      char nm[80];
+      const int n32_256 = (N / 32) * (N / 256), n16_128 = (N / 16) * (N / 128), n8_128 = (N / 8) * (N / 128);
+      snprintf(nm, sizeof nm, "kup8 32x256 grid %d", g);
+      t3([&] { st_full_items<32, 256, true><<<g, 256, 0, s>>>(K, N, ld, n32_256); }, nm);
+      snprintf(nm, sizeof nm, "col16B 32x256 grid %d", g);
+      t3([&] { st_full_items<32, 256, false><<<g, 256, 0, s>>>(K, N, ld, n32_256); }, nm);
+      snprintf(nm, sizeof nm, "col16B 16x128 grid %d", g);
+      t3([&] { st_full_items<16, 128, false><<<g, 256, 0, s>>>(K, N, ld, n16_128); }, nm);
+      snprintf(nm, sizeof nm, "col16B 8x128 grid %d", g);
+      t3([&] { st_full_items<8, 128, false><<<g, 256, 0, s>>>(K, N, ld, n8_128); }, nm);
+      snprintf(nm, sizeof nm, "kup8 16x128 grid %d", g);
+      t3([&] { st_full_items<16, 128, true><<<g, 256, 0, s>>>(K, N, ld, n16_128); }, nm);
+    }
     return 0;
   }
   struct Cfg { const char* name; std::vector<int> kinds; };

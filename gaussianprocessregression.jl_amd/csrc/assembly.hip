@@ -782,11 +782,19 @@ __global__ __launch_bounds__(256, 4) void kmat_crossg_kernel(KParams kp, const d
 // instruction writes 4 columns x 128 contiguous bytes -- no LDS staging.  Elements of the
 // diagonal blocks are computed in both orientations, bitwise equal: (2 y_i) y_j and (2 y_j) y_i
 // are the same products, summed over the same k order from the same C = -|y_i|^2 - |y_j|^2.
-constexpr int KU_W = 32;   // strip width (columns) = unit edge
+#ifndef KU_WIDTH  // columns per strip (16 or 32)
+#define KU_WIDTH 32
+#endif
+#ifndef KU_SEGROWS  // rows per work item
+#define KU_SEGROWS 128
+#endif
+constexpr int KU_W = KU_WIDTH;     // strip width (columns)
+constexpr int KU_CB = KU_W / 16;   // 16-column blocks per strip
+constexpr int KU_H = 32;           // unit height (rows): two 16-row blocks
 #ifndef KU_MINB  // workgroups (of 4 independent waves) per CU the upper-only build is compiled for
 #define KU_MINB 3
 #endif
-constexpr int KU_SEG = 256;  // rows per work item
+constexpr int KU_SEG = KU_SEGROWS;
 constexpr double KU_NC_LIM = 1.4e6;  // |y|^2 below which the exponentials need no clamp
 
 // rows of column block j0 the factorisation reads
@@ -799,7 +807,7 @@ __host__ __device__ inline int kup_rows(int j0, int n) { return min(n, 128 * (j0
 // masked.  Interior units store unconditionally, so the compiler counts the stores and the next
 // unit's prefetched operands are waited for with vmcnt(stores), not vmcnt(0).
 template <int S, int NSE, bool DIAG, bool EDGE, bool CLAMP>
-__device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[NSE][2][S],
+__device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[NSE][KU_CB][S],
                                          const double* cn, const double (&ra)[NSE][2][S],
                                          const double (&rn)[NSE][2], const double* tabs,
                                          double* __restrict__ K, size_t ldk, int i0, int j0,
@@ -813,7 +821,7 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
   // (200+ registers, one wave per SIMD); pinned one by one, the chains ran serially (each
   // exponential waited for its own table read)
   auto mfma_block = [&](int blk, gd4 (&acc)[NSE]) {
-    const int rb = blk >> 1, cb = blk & 1;
+    const int rb = blk / KU_CB, cb = blk % KU_CB;
 #pragma unroll
     for (int p = 0; p < NSE; ++p) {
 #pragma unroll
@@ -824,12 +832,13 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
         acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[p][cb][s], ra[p][rb][s], acc[p], 0, 0, 0);
     }
   };
+  constexpr int NBLK = 2 * KU_CB;
   gd4 acc[NSE], accn[NSE];
   mfma_block(0, acc);
 #pragma unroll
-  for (int blk = 0; blk < 4; ++blk) {
-    const int rb = blk >> 1, cb = blk & 1;
-    if (blk < 3) mfma_block(blk + 1, accn);
+  for (int blk = 0; blk < NBLK; ++blk) {
+    const int rb = blk / KU_CB, cb = blk % KU_CB;
+    if (blk < NBLK - 1) mfma_block(blk + 1, accn);
     double v[4];
 #pragma unroll
     for (int p = 0; p < NSE; ++p) {
@@ -840,7 +849,7 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
         double x = acc[p][q];  // -D
         bool on = false;
         if (DIAG) {
-          on = rb == cb && (lane & 15) == (lane >> 4) + 4 * q;
+          on = i0 + 16 * rb + (lane & 15) == j0 + 16 * cb + (lane >> 4) + 4 * q;
           if (on) x = 0.0;
         }
         e[q] = CLAMP ? kexp_s2(-x, ts) : kexp_s2_nc(-x, ts);
@@ -853,7 +862,8 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       double val = v[q];
-      if (DIAG && kp.has_noise && rb == cb && (lane & 15) == (lane >> 4) + 4 * q) val += kp.noise2;
+      if (DIAG && kp.has_noise && i0 + 16 * rb + (lane & 15) == j0 + 16 * cb + (lane >> 4) + 4 * q)
+        val += kp.noise2;
       // uniform base (SGPR) + the lane's 32-bit offset: rows 16 rb + (lane & 15), columns
       // 16 cb + 4 q + (lane >> 4) of the unit
       double* base = K + (size_t)(i0 + 16 * rb) + (size_t)(j0 + 16 * cb + 4 * q) * ldk;
@@ -864,7 +874,7 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
         __builtin_nontemporal_store(val, base + voff);
 #endif
     }
-    if (blk < 3)
+    if (blk < NBLK - 1)
 #pragma unroll
       for (int p = 0; p < NSE; ++p) acc[p] = accn[p];
   }
@@ -891,11 +901,11 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
     const int r1 = min(r0 + KU_SEG, full ? n : kup_rows(j0, n));
     // the strip's column operands (A role, registers) and column norms (this wave's LDS: the
     // lanes of a block read 4 distinct addresses per instruction -- broadcasts)
-    double ca[NSE][2][S];
+    double ca[NSE][KU_CB][S];
 #pragma unroll
     for (int p = 0; p < NSE; ++p)
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
+      for (int cb = 0; cb < KU_CB; ++cb) {
         const int bb = (j0 >> 4) + cb;
 #pragma unroll
         for (int s = 0; s < S; ++s) ca[p][cb][s] = gB[(((size_t)p * nblk + bb) * S + s) * 64 + lane];
@@ -915,7 +925,7 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
     __builtin_amdgcn_wave_barrier();
     // row operands (B role) of a 32-row unit: clamped to the last unit (branch-free prefetch)
     auto load_rows = [&](int i0, double (&ra)[NSE][2][S], double (&rn)[NSE][2]) {
-      const int ii = min(i0, r1 - 1) & ~(KU_W - 1);
+      const int ii = min(i0, r1 - 1) & ~(KU_H - 1);
 #pragma unroll
       for (int p = 0; p < NSE; ++p)
 #pragma unroll
@@ -929,17 +939,17 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
     double ra[NSE][2][S], rn[NSE][2];
     load_rows(r0, ra, rn);
     const bool edge_cols = j0 + KU_W > n;
-    for (int i0 = r0; i0 < r1; i0 += KU_W) {
+    for (int i0 = r0; i0 < r1; i0 += KU_H) {
       double nra[NSE][2][S], nrn[NSE][2];
-      load_rows(i0 + KU_W, nra, nrn);  // next unit's rows, in flight during this one
+      load_rows(i0 + KU_H, nra, nrn);  // next unit's rows, in flight during this one
       bool rbig = cols_big;
 #pragma unroll
       for (int p = 0; p < NSE; ++p) rbig |= !(-rn[p][0] < KU_NC_LIM) || !(-rn[p][1] < KU_NC_LIM);
       const bool clamp = __ballot(rbig) != 0;
       // (wave-uniform branches) the diagonal unit, ragged edges, the interior
-      if (i0 == j0)
+      if (j0 >= i0 && j0 < i0 + KU_H)  // (the unit holds diagonal elements)
         kup_unit<S, NSE, true, true, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
-      else if (edge_cols || i0 + KU_W > r1)
+      else if (edge_cols || i0 + KU_H > r1)
         kup_unit<S, NSE, false, true, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);
       else if (clamp)
         kup_unit<S, NSE, false, false, true>(kp, ca, cn, ra, rn, tabs, K, ldk, i0, j0, r1, n, voff);

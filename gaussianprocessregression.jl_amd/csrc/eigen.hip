@@ -78,7 +78,54 @@ __device__ __forceinline__ void gemm64(const double* X, const double* Y, double 
   }
 }
 
-// 1. per pair: diagonalise S = A[P, P] by parallel Jacobi in LDS, R = accumulated rotation
+typedef double ed4 __attribute__((ext_vector_type(4)));
+
+// The same 64 x 64 product on the FP64 matrix cores: wave w owns the 32 x 32 quadrant rows
+// 32 (w & 1).., columns 32 (w >> 1)..; v_mfma_f64_16x16x4f64 takes lane l's A[l & 15][l >> 4]
+// and B[l >> 4][l & 15] and leaves C[(l >> 4) + 4 q][l & 15] in register q.  Written into Z
+// (LDS, row stride ELD) -- Z may alias X or Y: the barrier before the stores orders them after
+// every wave's last operand read.
+template <bool TA>
+__device__ __forceinline__ void gemm64_mfma(const double* X, const double* Y, double* Z) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = 32 * (w & 1), c0 = 32 * (w >> 1);
+  ed4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = ed4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int ks = 0; ks < ES / 4; ++ks) {
+    const int k = 4 * ks + (lane >> 4);
+    double xa[2], yb[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int i = r0 + 16 * a + (lane & 15);
+      xa[a] = TA ? X[k + i * ELD] : X[i + k * ELD];
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) yb[b] = Y[k + (c0 + 16 * b + (lane & 15)) * ELD];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a], yb[b], acc[a][b], 0, 0, 0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        Z[(r0 + 16 * a + (lane >> 4) + 4 * q) + (c0 + 16 * b + (lane & 15)) * ELD] = acc[a][b][q];
+  __syncthreads();
+}
+
+// 1. per pair: diagonalise S = A[P, P] by parallel Jacobi in LDS, R = accumulated rotation.
+//    MERGED: each step's two-sided update in one pass over 2 x 2 blocks (GPR_EIG_SUBK=1; the
+//    two-pass form gives bitwise the same S and R)
+template <bool MERGED>
 __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __restrict__ A, size_t lda,
                                                             int nb, int round,
                                                             double* __restrict__ Rbuf,
@@ -125,6 +172,47 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
         pr[t][1] = q;
       }
       __syncthreads();
+      if (MERGED) {
+        // S <- J^T S J by 2 x 2 blocks (row pair a, column pair b): the row rotation, then the
+        // column rotation of the row-rotated values -- the same operations in the same order
+        // as the two passes below, one barrier and half the LDS traffic fewer
+        const int b = t & 31;
+        const double cb = cs[b][0], sb = cs[b][1];
+        const int pb = pr[b][0], qb = pr[b][1];
+#pragma unroll
+        for (int a = t >> 5; a < ES / 2; a += 8) {
+          const double ca = cs[a][0], sa = cs[a][1];
+          if (sa == 0.0 && sb == 0.0) continue;
+          const int pa = pr[a][0], qa = pr[a][1];
+          double x00 = S[pa + pb * ELD], x01 = S[pa + qb * ELD];
+          double x10 = S[qa + pb * ELD], x11 = S[qa + qb * ELD];
+          if (sa != 0.0) {
+            const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
+            const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
+            x00 = y00; x10 = y10; x01 = y01; x11 = y11;
+          }
+          if (sb != 0.0) {
+            const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
+            const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
+            x00 = y00; x01 = y01; x10 = y10; x11 = y11;
+          }
+          S[pa + pb * ELD] = x00;
+          S[pa + qb * ELD] = x01;
+          S[qa + pb * ELD] = x10;
+          S[qa + qb * ELD] = x11;
+        }
+        for (int e = t; e < (ES / 2) * ES; e += 256) {
+          const int pk = e / ES, i = e % ES;
+          const double c = cs[pk][0], s = cs[pk][1];
+          if (s == 0.0) continue;
+          const int p = pr[pk][0], q = pr[pk][1];
+          const double rp = R[i + p * ELD], rq = R[i + q * ELD];
+          R[i + p * ELD] = c * rp - s * rq;
+          R[i + q * ELD] = s * rp + c * rq;
+        }
+        __syncthreads();
+        continue;
+      }
       // rows p, q of S: S <- J^T S   (J: c at (p,p), (q,q); s at (p,q); -s at (q,p))
       for (int e = t; e < (ES / 2) * ES; e += 256) {
         const int pk = e / ES, j = e % ES;
@@ -189,6 +277,9 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
 
 // 2. A[P_k, P_l] <- R_k^T A[P_k, P_l] R_l for every tile k <= l (mirrored into (l, k)), and
 //    B[P_k, cols] <- R_k^T B[P_k, cols] for every pair k and 64-column chunk of B
+//    MF: the two products on the matrix cores, staged through LDS and stored by columns
+//    (GPR_EIG_TMFMA=1; else the VALU form)
+template <bool MF>
 __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__ A, size_t lda,
                                                            int nb, int round,
                                                            const double* __restrict__ Rbuf,
@@ -220,6 +311,22 @@ __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__
       Rk[i + j * ELD] = Rkg[e];
     }
     __syncthreads();
+    if (MF) {
+      gemm64_mfma<false>(T, Rl, U);  // U = T R_l
+      gemm64_mfma<true>(Rk, U, T);   // T = R_k^T U
+      // column runs of 32 contiguous rows (the pair's two blocks) per 64-lane store
+      for (int e = t; e < ES * ES; e += 256) {
+        const int i = e % ES, j = e / ES;
+        const double v = (k == l && i > j) ? T[j + i * ELD] : T[i + j * ELD];
+        A[(size_t)pair_row(Ik, Jk, i) + (size_t)pair_row(Il, Jl, j) * lda] = v;
+      }
+      if (k != l)  // the mirror (l, k): its column j is row j of T
+        for (int e = t; e < ES * ES; e += 256) {
+          const int i = e % ES, j = e / ES;
+          A[(size_t)pair_row(Il, Jl, i) + (size_t)pair_row(Ik, Jk, j) * lda] = T[j + i * ELD];
+        }
+      return;
+    }
     double c[4][4];
     gemm64<false>(T, Rl, c);  // U = T R_l
 #pragma unroll
@@ -265,6 +372,14 @@ __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__
     Rk[i + j * ELD] = Rkg[e];
   }
   __syncthreads();
+  if (MF) {
+    gemm64_mfma<true>(Rk, T, U);
+    for (int e = t; e < ES * ES; e += 256) {
+      const int i = e % ES, j = e / ES, col = ch * ES + j;
+      if (col < m) B[(size_t)pair_row(Ik, Jk, i) + (size_t)col * ldb] = U[i + j * ELD];
+    }
+    return;
+  }
   double c[4][4];
   gemm64<true>(Rk, T, c);
 #pragma unroll
@@ -321,15 +436,24 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
   static const int max_sweeps = getenv("GPR_EIG_MAX_SWEEPS") ? atoi(getenv("GPR_EIG_MAX_SWEEPS")) : 60;
   static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 1;
   static const int reorth = getenv("GPR_EIG_REORTH") ? atoi(getenv("GPR_EIG_REORTH")) : 1;
+  static const bool merged = getenv("GPR_EIG_SUBK") ? atoi(getenv("GPR_EIG_SUBK")) != 0 : false;
+  static const bool tmfma = getenv("GPR_EIG_TMFMA") ? atoi(getenv("GPR_EIG_TMFMA")) != 0 : false;
   const int nch = m > 0 ? (m + ES - 1) / ES : 0;
   int sweep = 0, hrot = 1;
   TimerScope ts(ctx, TC_OTHER, 0.0);
   for (; sweep < max_sweeps && hrot; ++sweep) {
     HIP_TRY(ctx, hipMemsetAsync(rot, 0, sizeof(int), s));
     for (int r = 0; r < nb - 1; ++r) {
-      eig_subproblem_kernel<<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
-      eig_transform_kernel<<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
-                                                                (size_t)n2, m, ntiles);
+      if (merged)
+        eig_subproblem_kernel<true><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
+      else
+        eig_subproblem_kernel<false><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
+      if (tmfma)
+        eig_transform_kernel<true><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
+                                                                    (size_t)n2, m, ntiles);
+      else
+        eig_transform_kernel<false><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
+                                                                     (size_t)n2, m, ntiles);
     }
     LAUNCH_CHECK(ctx);
     HIP_TRY(ctx, hipMemcpyAsync(&hrot, rot, sizeof(int), hipMemcpyDeviceToHost, s));

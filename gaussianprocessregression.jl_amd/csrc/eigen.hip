@@ -272,7 +272,10 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
   }
   double* Rk = Rbuf + (size_t)k * ES * ES;
   for (int e = t; e < ES * ES; e += 256) Rk[e] = R[(e % ES) + (e / ES) * ELD];
-  if (t == 0 && rot_total) atomicAdd(rotations, rot_total);
+  if (t == 0) {
+    if (rot_total) atomicAdd(rotations, rot_total);
+    rotations[2 + k] = rot_total != 0;  // R_k != I: the transform skips identity factors
+  }
 }
 
 // 2. A[P_k, P_l] <- R_k^T A[P_k, P_l] R_l for every tile k <= l (mirrored into (l, k)), and
@@ -284,7 +287,8 @@ __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__
                                                            int nb, int round,
                                                            const double* __restrict__ Rbuf,
                                                            double* __restrict__ B, size_t ldb,
-                                                           int m, int ntiles) {
+                                                           int m, int ntiles,
+                                                           const int* __restrict__ rflag) {
   __shared__ double lds[4 * ES * ELD];  // 133 KB: one workgroup per CU
   double* T = lds;               // tile (then U = T R_l)
   double* Rl = T + ES * ELD;
@@ -299,6 +303,10 @@ __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__
     while ((l + 1) * (l + 2) / 2 <= bid) ++l;
     while (l * (l + 1) / 2 > bid) --l;
     const int k = bid - l * (l + 1) / 2;
+    // a pair that rotated nothing this round has R = I exactly, and a product with I is exact
+    // (every other term is a signed zero): such factors are skipped, bitwise the same result
+    const bool fk = !rflag || rflag[k] != 0, fl = !rflag || rflag[l] != 0;
+    if (!fk && !fl) return;
     int Ik, Jk, Il, Jl;
     circle_pair(nb, round, k, &Ik, &Jk);
     circle_pair(nb, round, l, &Il, &Jl);
@@ -312,18 +320,25 @@ __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__
     }
     __syncthreads();
     if (MF) {
-      gemm64_mfma<false>(T, Rl, U);  // U = T R_l
-      gemm64_mfma<true>(Rk, U, T);   // T = R_k^T U
+      double* res = T;
+      if (fl) {
+        gemm64_mfma<false>(T, Rl, U);  // U = T R_l
+        res = U;
+      }
+      if (fk) {
+        gemm64_mfma<true>(Rk, res, T);  // T = R_k^T U
+        res = T;
+      }
       // column runs of 32 contiguous rows (the pair's two blocks) per 64-lane store
       for (int e = t; e < ES * ES; e += 256) {
         const int i = e % ES, j = e / ES;
-        const double v = (k == l && i > j) ? T[j + i * ELD] : T[i + j * ELD];
+        const double v = (k == l && i > j) ? res[j + i * ELD] : res[i + j * ELD];
         A[(size_t)pair_row(Ik, Jk, i) + (size_t)pair_row(Il, Jl, j) * lda] = v;
       }
       if (k != l)  // the mirror (l, k): its column j is row j of T
         for (int e = t; e < ES * ES; e += 256) {
           const int i = e % ES, j = e / ES;
-          A[(size_t)pair_row(Il, Jl, i) + (size_t)pair_row(Ik, Jk, j) * lda] = T[j + i * ELD];
+          A[(size_t)pair_row(Il, Jl, i) + (size_t)pair_row(Ik, Jk, j) * lda] = res[j + i * ELD];
         }
       return;
     }
@@ -362,7 +377,7 @@ __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__
   bid -= ntiles;
   const int nch = (m + ES - 1) / ES;
   const int k = bid / nch, ch = bid % nch;
-  if (k >= np) return;
+  if (k >= np || (rflag && !rflag[k])) return;
   int Ik, Jk;
   circle_pair(nb, round, k, &Ik, &Jk);
   const double* Rkg = Rbuf + (size_t)k * ES * ES;
@@ -419,12 +434,12 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
   const int nb = n2 / EB, np = nb / 2;
   const int ntiles = np * (np + 1) / 2;
   // workspace: W (n2 x n2), Bp (n2 x m), R (np x 64 x 64), rotation counter
-  const size_t need = (size_t)n2 * n2 + (size_t)n2 * std::max(m, 1) + (size_t)np * ES * ES + 1;
+  const size_t need = (size_t)n2 * n2 + (size_t)n2 * std::max(m, 1) + (size_t)np * ES * ES + 2 + np;
   GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
   double* W = ctx->deig;
   double* Bp = W + (size_t)n2 * n2;
   double* Rb = Bp + (size_t)n2 * std::max(m, 1);
-  int* rot = reinterpret_cast<int*>(Rb + (size_t)np * ES * ES);
+  int* rot = reinterpret_cast<int*>(Rb + (size_t)np * ES * ES);  // [0] count, [2 + k] flags
   hipStream_t s = ctx->stream;
   eig_pad_kernel<<<1024, 256, 0, s>>>(dA, (size_t)lda, n, W, n2);
   LAUNCH_CHECK(ctx);
@@ -438,6 +453,7 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
   static const int reorth = getenv("GPR_EIG_REORTH") ? atoi(getenv("GPR_EIG_REORTH")) : 1;
   static const bool merged = getenv("GPR_EIG_SUBK") ? atoi(getenv("GPR_EIG_SUBK")) != 0 : false;
   static const bool tmfma = getenv("GPR_EIG_TMFMA") ? atoi(getenv("GPR_EIG_TMFMA")) != 0 : false;
+  static const bool skipi = getenv("GPR_EIG_SKIPI") ? atoi(getenv("GPR_EIG_SKIPI")) != 0 : false;
   const int nch = m > 0 ? (m + ES - 1) / ES : 0;
   int sweep = 0, hrot = 1;
   TimerScope ts(ctx, TC_OTHER, 0.0);
@@ -450,10 +466,10 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
         eig_subproblem_kernel<false><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
       if (tmfma)
         eig_transform_kernel<true><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
-                                                                    (size_t)n2, m, ntiles);
+                                                                    (size_t)n2, m, ntiles, skipi ? rot + 2 : nullptr);
       else
         eig_transform_kernel<false><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
-                                                                     (size_t)n2, m, ntiles);
+                                                                     (size_t)n2, m, ntiles, skipi ? rot + 2 : nullptr);
     }
     LAUNCH_CHECK(ctx);
     HIP_TRY(ctx, hipMemcpyAsync(&hrot, rot, sizeof(int), hipMemcpyDeviceToHost, s));

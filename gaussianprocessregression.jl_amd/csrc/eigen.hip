@@ -22,9 +22,9 @@
 // accuracy) or when the angle is below rounding (|tan| < 1e-17), so a converged matrix is
 // left exactly as it is (R = I is applied exactly).
 //
-// Cost: per round one small latency-bound launch (nb/2 workgroups) and one pass over K
-// (16 n^2 bytes, 2 x 64^3 FMAs per tile on the VALU, register-blocked 4 x 4 per thread);
-// nb - 1 rounds per sweep, ~6-10 sweeps.
+// Cost: per round one small latency-bound launch (nb/2 workgroups, 63 dependent steps: ~95 us,
+// ~70 % of the time) and one pass over K (16 n^2 bytes, 2 x 64^3 FP64 MFMA per tile, ~38 us);
+// nb - 1 rounds per sweep, 9-25 sweeps (n = 1100: 56 ms random, 110 ms SE kernel).
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -123,10 +123,13 @@ __device__ __forceinline__ void gemm64_mfma(const double* X, const double* Y, do
 }
 
 // 1. per pair: diagonalise S = A[P, P] by parallel Jacobi in LDS, R = accumulated rotation.
-//    MERGED: each step's two-sided update in one pass over 2 x 2 blocks (GPR_EIG_SUBK=1; the
-//    two-pass form gives bitwise the same S and R)
-template <bool MERGED>
-__global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __restrict__ A, size_t lda,
+//    MERGED (default; GPR_EIG_SUBK=0 selects the first form: two passes, 256 threads, rotations
+//    skipped by branches): 1024 threads, one 2 x 2 block of S and two entries of R each; per
+//    step the rotations from one division and two square roots, then S's two-sided update and
+//    R's in one straight-line pass, one barrier each.  Same box, n = 1100: 165 -> 95 us per
+//    launch (profiles/r04_eig_speed.txt)
+template <bool MERGED, int NT>
+__global__ __launch_bounds__(NT) void eig_subproblem_kernel(const double* __restrict__ A, size_t lda,
                                                             int nb, int round,
                                                             double* __restrict__ Rbuf,
                                                             int* __restrict__ rotations,
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
   const int k = blockIdx.x, t = threadIdx.x;
   int I, J;
   circle_pair(nb, round, k, &I, &J);
-  for (int e = t; e < ES * ES; e += 256) {
+  for (int e = t; e < ES * ES; e += NT) {
     const int i = e % ES, j = e / ES;
     S[i + j * ELD] = A[(size_t)pair_row(I, J, i) + (size_t)pair_row(I, J, j) * lda];
     R[i + j * ELD] = i == j ? 1.0 : 0.0;
@@ -150,6 +153,72 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
     if (t == 0) rot_sweep = 0;
     __syncthreads();
     for (int step = 0; step < ES - 1; ++step) {
+      if (MERGED) {
+        // rotations: wave 0, lane t < 32 for pair t.  t = tan of the angle that zeroes s_pq,
+        // Rutishauser's root sign(theta) / (|theta| + sqrt(1 + theta^2)), theta = (s_qq -
+        // s_pp) / (2 s_pq), written with one division: |h| / (|d| + sqrt(d^2 + h^2)), d = s_qq -
+        // s_pp, h = 2 s_pq; the skip test squared (no square root)
+        if (t < 64) {
+          bool rot = false;
+          if (t < ES / 2) {
+            int p, q;
+            circle_pair(ES, step, t, &p, &q);
+            if (p > q) { const int w = p; p = q; q = w; }
+            const double app = S[p + p * ELD], aqq = S[q + q * ELD], apq = S[p + q * ELD];
+            double c = 1.0, s = 0.0;
+            if (apq != 0.0 && apq * apq > 1e-30 * fabs(app * aqq)) {
+              const double d = aqq - app, h = 2.0 * apq;
+              const bool pos = d == 0.0 || ((d > 0.0) == (h > 0.0));
+              const double ah = pos ? fabs(h) : -fabs(h);
+              const double tt = ah / (fabs(d) + sqrt(fma(d, d, h * h)));
+              if (fabs(tt) >= 1e-17) {
+                c = 1.0 / sqrt(fma(tt, tt, 1.0));
+                s = tt * c;
+                rot = true;
+              }
+            }
+            cs[t][0] = c;
+            cs[t][1] = s;
+            pr[t][0] = p;
+            pr[t][1] = q;
+          }
+          const unsigned long long m = __ballot(rot);
+          if (t == 0 && m) rot_sweep += __popcll(m);
+        }
+        __syncthreads();
+        // S <- J^T S J by 2 x 2 blocks (row pair a, column pair b: the row rotation, then the
+        // column rotation of the row-rotated values) and R <- R J, straight-line: a pair that
+        // did not rotate has c = 1, s = 0, which leaves every value exactly as it is
+        const int b = t & 31;
+        const double cb = cs[b][0], sb = cs[b][1];
+        const int pb = pr[b][0], qb = pr[b][1];
+#pragma unroll
+        for (int u = 0; u < 1024 / NT; ++u) {
+          const int a = (t >> 5) + (NT / 32) * u;
+          const double ca = cs[a][0], sa = cs[a][1];
+          const int pa = pr[a][0], qa = pr[a][1];
+          const double x00 = S[pa + pb * ELD], x01 = S[pa + qb * ELD];
+          const double x10 = S[qa + pb * ELD], x11 = S[qa + qb * ELD];
+          const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
+          const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
+          S[pa + pb * ELD] = cb * y00 - sb * y01;
+          S[pa + qb * ELD] = sb * y00 + cb * y01;
+          S[qa + pb * ELD] = cb * y10 - sb * y11;
+          S[qa + qb * ELD] = sb * y10 + cb * y11;
+        }
+        const int i = t & 63;
+#pragma unroll
+        for (int u = 0; u < 2048 / NT; ++u) {
+          const int pk = (t >> 6) + (NT / 64) * u;
+          const double c = cs[pk][0], s = cs[pk][1];
+          const int p = pr[pk][0], q = pr[pk][1];
+          const double rp = R[i + p * ELD], rq = R[i + q * ELD];
+          R[i + p * ELD] = c * rp - s * rq;
+          R[i + q * ELD] = s * rp + c * rq;
+        }
+        __syncthreads();
+        continue;
+      }
       if (t < ES / 2) {
         int p, q;
         circle_pair(ES, step, t, &p, &q);
@@ -172,49 +241,8 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
         pr[t][1] = q;
       }
       __syncthreads();
-      if (MERGED) {
-        // S <- J^T S J by 2 x 2 blocks (row pair a, column pair b): the row rotation, then the
-        // column rotation of the row-rotated values -- the same operations in the same order
-        // as the two passes below, one barrier and half the LDS traffic fewer
-        const int b = t & 31;
-        const double cb = cs[b][0], sb = cs[b][1];
-        const int pb = pr[b][0], qb = pr[b][1];
-#pragma unroll
-        for (int a = t >> 5; a < ES / 2; a += 8) {
-          const double ca = cs[a][0], sa = cs[a][1];
-          if (sa == 0.0 && sb == 0.0) continue;
-          const int pa = pr[a][0], qa = pr[a][1];
-          double x00 = S[pa + pb * ELD], x01 = S[pa + qb * ELD];
-          double x10 = S[qa + pb * ELD], x11 = S[qa + qb * ELD];
-          if (sa != 0.0) {
-            const double y00 = ca * x00 - sa * x10, y10 = sa * x00 + ca * x10;
-            const double y01 = ca * x01 - sa * x11, y11 = sa * x01 + ca * x11;
-            x00 = y00; x10 = y10; x01 = y01; x11 = y11;
-          }
-          if (sb != 0.0) {
-            const double y00 = cb * x00 - sb * x01, y01 = sb * x00 + cb * x01;
-            const double y10 = cb * x10 - sb * x11, y11 = sb * x10 + cb * x11;
-            x00 = y00; x01 = y01; x10 = y10; x11 = y11;
-          }
-          S[pa + pb * ELD] = x00;
-          S[pa + qb * ELD] = x01;
-          S[qa + pb * ELD] = x10;
-          S[qa + qb * ELD] = x11;
-        }
-        for (int e = t; e < (ES / 2) * ES; e += 256) {
-          const int pk = e / ES, i = e % ES;
-          const double c = cs[pk][0], s = cs[pk][1];
-          if (s == 0.0) continue;
-          const int p = pr[pk][0], q = pr[pk][1];
-          const double rp = R[i + p * ELD], rq = R[i + q * ELD];
-          R[i + p * ELD] = c * rp - s * rq;
-          R[i + q * ELD] = s * rp + c * rq;
-        }
-        __syncthreads();
-        continue;
-      }
       // rows p, q of S: S <- J^T S   (J: c at (p,p), (q,q); s at (p,q); -s at (q,p))
-      for (int e = t; e < (ES / 2) * ES; e += 256) {
+      for (int e = t; e < (ES / 2) * ES; e += NT) {
         const int pk = e / ES, j = e % ES;
         const double c = cs[pk][0], s = cs[pk][1];
         if (s == 0.0) continue;
@@ -225,7 +253,7 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
       }
       __syncthreads();
       // columns p, q of S and of R: S <- S J, R <- R J
-      for (int e = t; e < (ES / 2) * ES; e += 256) {
+      for (int e = t; e < (ES / 2) * ES; e += NT) {
         const int pk = e / ES, i = e % ES;
         const double c = cs[pk][0], s = cs[pk][1];
         if (s == 0.0) continue;
@@ -248,30 +276,36 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
   // applied round after round, that drift (not the rotations' own rounding) set the
   // eigenvalue error.  One Newton-Schulz step R <- R (3 I - R^T R) / 2 takes it to rounding
   // level (quadratic: 1e-14 -> 1e-28) -- two 64^3 products in LDS, S's space holding R^T R.
-  if (reorth && rot_total) {
-    const int i0 = 4 * (t % 16), j0 = 4 * (t / 16);
+  if (reorth && rot_total) {  // (the products on the first 256 threads)
+    const bool on = t < 256;
+    const int i0 = 4 * (t % 16), j0 = 4 * ((t / 16) % 16);
     double c[4][4];
-    gemm64<true>(R, R, c);
+    if (on) {
+      gemm64<true>(R, R, c);
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) S[(i0 + a) + (j0 + b) * ELD] = c[a][b];
+        for (int b = 0; b < 4; ++b) S[(i0 + a) + (j0 + b) * ELD] = c[a][b];
+    }
     __syncthreads();
-    gemm64<false>(R, S, c);  // R (R^T R)
     double r[4][4];
+    if (on) {
+      gemm64<false>(R, S, c);  // R (R^T R)
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) r[a][b] = 1.5 * R[(i0 + a) + (j0 + b) * ELD] - 0.5 * c[a][b];
+        for (int b = 0; b < 4; ++b) r[a][b] = 1.5 * R[(i0 + a) + (j0 + b) * ELD] - 0.5 * c[a][b];
+    }
     __syncthreads();
+    if (on)
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) R[(i0 + a) + (j0 + b) * ELD] = r[a][b];
+        for (int b = 0; b < 4; ++b) R[(i0 + a) + (j0 + b) * ELD] = r[a][b];
     __syncthreads();
   }
   double* Rk = Rbuf + (size_t)k * ES * ES;
-  for (int e = t; e < ES * ES; e += 256) Rk[e] = R[(e % ES) + (e / ES) * ELD];
+  for (int e = t; e < ES * ES; e += NT) Rk[e] = R[(e % ES) + (e / ES) * ELD];
   if (t == 0) {
     if (rot_total) atomicAdd(rotations, rot_total);
     rotations[2 + k] = rot_total != 0;  // R_k != I: the transform skips identity factors
@@ -281,7 +315,8 @@ __global__ __launch_bounds__(256) void eig_subproblem_kernel(const double* __res
 // 2. A[P_k, P_l] <- R_k^T A[P_k, P_l] R_l for every tile k <= l (mirrored into (l, k)), and
 //    B[P_k, cols] <- R_k^T B[P_k, cols] for every pair k and 64-column chunk of B
 //    MF: the two products on the matrix cores, staged through LDS and stored by columns
-//    (GPR_EIG_TMFMA=1; else the VALU form)
+//    (default; GPR_EIG_TMFMA=0: the VALU form).  rflag (default; GPR_EIG_SKIPI=0 passes null):
+//    the pairs that rotated this round -- identity factors are skipped
 template <bool MF>
 __global__ __launch_bounds__(256) void eig_transform_kernel(double* __restrict__ A, size_t lda,
                                                            int nb, int round,
@@ -451,9 +486,9 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
   static const int max_sweeps = getenv("GPR_EIG_MAX_SWEEPS") ? atoi(getenv("GPR_EIG_MAX_SWEEPS")) : 60;
   static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 1;
   static const int reorth = getenv("GPR_EIG_REORTH") ? atoi(getenv("GPR_EIG_REORTH")) : 1;
-  static const bool merged = getenv("GPR_EIG_SUBK") ? atoi(getenv("GPR_EIG_SUBK")) != 0 : false;
-  static const bool tmfma = getenv("GPR_EIG_TMFMA") ? atoi(getenv("GPR_EIG_TMFMA")) != 0 : false;
-  static const bool skipi = getenv("GPR_EIG_SKIPI") ? atoi(getenv("GPR_EIG_SKIPI")) != 0 : false;
+  static const bool merged = getenv("GPR_EIG_SUBK") ? atoi(getenv("GPR_EIG_SUBK")) != 0 : true;
+  static const bool tmfma = getenv("GPR_EIG_TMFMA") ? atoi(getenv("GPR_EIG_TMFMA")) != 0 : true;
+  static const bool skipi = getenv("GPR_EIG_SKIPI") ? atoi(getenv("GPR_EIG_SKIPI")) != 0 : true;
   const int nch = m > 0 ? (m + ES - 1) / ES : 0;
   int sweep = 0, hrot = 1;
   TimerScope ts(ctx, TC_OTHER, 0.0);
@@ -461,9 +496,9 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
     HIP_TRY(ctx, hipMemsetAsync(rot, 0, sizeof(int), s));
     for (int r = 0; r < nb - 1; ++r) {
       if (merged)
-        eig_subproblem_kernel<true><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
+        eig_subproblem_kernel<true, 1024><<<np, 1024, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
       else
-        eig_subproblem_kernel<false><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
+        eig_subproblem_kernel<false, 256><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
       if (tmfma)
         eig_transform_kernel<true><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
                                                                     (size_t)n2, m, ntiles, skipi ? rot + 2 : nullptr);

@@ -309,9 +309,11 @@ int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int
                  int ldb, double* norm_out, int lower_rhs);
 int kinv_from_z(gpr_ctx* ctx, const double* Z, int n, double* dKinv, int ldk);
 // symmetric eigendecomposition A = P diag(lam) P^T applied to B: lam (n, device) and
-// B <- P^T B (n x m, ld ldb), A read only (eigen.hip, block Jacobi); *sweeps may be null
+// B <- P^T B (n x m, ld ldb), A read only (eigen.hip, block Jacobi); *sweeps may be null.
+// floor >= 0: the eigenvalues of A + floor I to high relative accuracy (what (lam + s)^-1 needs
+// for every s >= floor); 0 = those of A itself
 int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
-                  double* dlam, int* sweeps);
+                  double* dlam, int* sweeps, double floor = 0.0);
 // norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream
 int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm);
 // forward = false: only the backward sweep U x = B (B already holds U^{-T} b);

@@ -17,10 +17,12 @@
 //      k <= l and mirrored, so K stays exactly symmetric) and the pair's rows of B become
 //      R_k^T B[P_k, :] -- all pairs' transforms at once, J^T K J with J = diag(R_k).
 // A sweep that rotates nothing anywhere ends it: lambda = diag(K), B = P^T B_in.  Rotations
-// follow Rutishauser's stable formulas and are skipped when |s_pq| <= 1e-15 sqrt(|s_pp s_qq|)
-// (the Demmel-Veselic criterion: eigenvalues of a positive definite K to high relative
-// accuracy) or when the angle is below rounding (|tan| < 1e-17), so a converged matrix is
-// left exactly as it is (R = I is applied exactly).
+// follow Rutishauser's stable formulas and are skipped when |s_pq| <= 1e-15 sqrt((|s_pp| + f)
+// (|s_qq| + f)) (the Demmel-Veselic criterion for K + f I: its eigenvalues to high relative
+// accuracy -- f = 0 for K itself; the quadrature passes f = its smallest nonnegative shift,
+// which is all (lambda + s)^-1 needs for every shift s >= f) or when the angle is below
+// rounding (|tan| < 1e-17), so a converged matrix is left exactly as it is (R = I is applied
+// exactly).
 //
 // Cost: per round one small latency-bound launch (nb/2 workgroups, 63 dependent steps: ~95 us,
 // ~70 % of the time) and one pass over K (16 n^2 bytes, 2 x 64^3 FP64 MFMA per tile, ~38 us);
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(NT) void eig_subproblem_kernel(const double* __rest
                                                             int nb, int round,
                                                             double* __restrict__ Rbuf,
                                                             int* __restrict__ rotations,
-                                                            int max_inner, int reorth) {
+                                                            int max_inner, int reorth, double sig) {
   __shared__ double S[ES * ELD];
   __shared__ double R[ES * ELD];
   __shared__ double cs[ES / 2][2];
@@ -149,6 +151,26 @@ __global__ __launch_bounds__(NT) void eig_subproblem_kernel(const double* __rest
   }
   if (t == 0) rot_total = 0;
   __syncthreads();
+  if (MERGED) {
+    // a pair none of whose off-diagonal entries passes the rotation test rotates nothing this
+    // round (its S would stay exactly as it is): R = I, flag 0, no 63-step sweep -- in the
+    // late sweeps most pairs
+    bool need = false;
+    for (int e = t; e < ES * ES; e += NT) {
+      const int i = e % ES, j = e / ES;
+      if (i < j) {
+        const double apq = S[i + j * ELD];
+        need |= apq != 0.0 &&
+                apq * apq > 1e-30 * ((fabs(S[i + i * ELD]) + sig) * (fabs(S[j + j * ELD]) + sig));
+      }
+    }
+    if (!__syncthreads_or(need)) {
+      double* Rk = Rbuf + (size_t)k * ES * ES;
+      for (int e = t; e < ES * ES; e += NT) Rk[e] = (e % ES) == (e / ES) ? 1.0 : 0.0;
+      if (t == 0) rotations[2 + k] = 0;
+      return;
+    }
+  }
   for (int sweep = 0; sweep < max_inner; ++sweep) {
     if (t == 0) rot_sweep = 0;
     __syncthreads();
@@ -166,7 +188,7 @@ __global__ __launch_bounds__(NT) void eig_subproblem_kernel(const double* __rest
             if (p > q) { const int w = p; p = q; q = w; }
             const double app = S[p + p * ELD], aqq = S[q + q * ELD], apq = S[p + q * ELD];
             double c = 1.0, s = 0.0;
-            if (apq != 0.0 && apq * apq > 1e-30 * fabs(app * aqq)) {
+            if (apq != 0.0 && apq * apq > 1e-30 * ((fabs(app) + sig) * (fabs(aqq) + sig))) {
               const double d = aqq - app, h = 2.0 * apq;
               const bool pos = d == 0.0 || ((d > 0.0) == (h > 0.0));
               const double ah = pos ? fabs(h) : -fabs(h);
@@ -463,7 +485,7 @@ __global__ void eig_diag_kernel(const double* __restrict__ W, int n2, int n, dou
 // B's rows in the same order.  *sweeps: outer sweeps used.  Returns GPR_E_HIP (with a message)
 // if the iteration does not converge within GPR_EIG_MAX_SWEEPS (default 60).
 int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
-                  double* dlam, int* sweeps_out) {
+                  double* dlam, int* sweeps_out, double floor) {
   if (n <= 0) return 0;
   const int n2 = (n + ES - 1) / ES * ES;
   const int nb = n2 / EB, np = nb / 2;
@@ -496,9 +518,9 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
     HIP_TRY(ctx, hipMemsetAsync(rot, 0, sizeof(int), s));
     for (int r = 0; r < nb - 1; ++r) {
       if (merged)
-        eig_subproblem_kernel<true, 1024><<<np, 1024, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
+        eig_subproblem_kernel<true, 1024><<<np, 1024, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth, floor);
       else
-        eig_subproblem_kernel<false, 256><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth);
+        eig_subproblem_kernel<false, 256><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth, 0.0);
       if (tmfma)
         eig_transform_kernel<true><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
                                                                     (size_t)n2, m, ntiles, skipi ? rot + 2 : nullptr);

@@ -793,7 +793,10 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
                                 ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise, sizeof(double) * ny, hipMemcpyHostToDevice,
                                 ctx->stream));
-    GPR_TRY(sym_eig_apply(ctx, K, n, n, T, ny + 1, n, lam, nullptr));
+    // relative accuracy for K + s_min I (s_min = the smallest shift when none is negative)
+    double smin = noise[0];
+    for (int j = 1; j < ny; ++j) smin = std::min(smin, noise[j]);
+    GPR_TRY(sym_eig_apply(ctx, K, n, n, T, ny + 1, n, lam, nullptr, std::max(smin, 0.0)));
     quad_diag_update_kernel<<<ny, 256, 0, ctx->stream>>>(T, n, ny, lam, dnoise, k2, out);
     LAUNCH_CHECK(ctx);
     std::vector<double> h(2 * (size_t)ny);
@@ -888,8 +891,20 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   // Jacobi eigensolver.  GPR_QUAD_EIGEN=0: K + noise_j I factored per column (PD shifts only);
   // =2: rocSOLVER's dsyevd for the decomposition (timing comparator; falls back to the
   // per-column factorisations when it cannot be loaded)
+  // Unset: per-column factorisations when every shift is nonnegative (K + s I is then positive
+  // definite) and ny of them cost less than one eigendecomposition (measured crossover,
+  // profiles/r04_eig_speed.txt: ~ny < n / 8 + 64), else the eigensolver; a per-column path that
+  // meets a non-positive-definite K + s I falls back to the eigensolver.  =1 forces the
+  // eigensolver.
   const char* qe = getenv("GPR_QUAD_EIGEN");
-  const int qmode = qe ? atoi(qe) : 1;
+  int qmode = qe ? atoi(qe) : -1;
+  bool fallback = false;
+  if (qmode < 0) {
+    double smin = noise[0];
+    for (int j = 1; j < ny; ++j) smin = std::min(smin, noise[j]);
+    qmode = (smin >= 0.0 && ny < n / 8 + 64) ? 0 : 1;
+    fallback = qmode == 0;
+  }
   if (qmode != 0) {
     const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode == 2);
     if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
@@ -897,14 +912,20 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);
   if (n > 8192) nsub = 1;
   nsub = cap_children_by_memory(nsub, ((size_t)n * n + 2 * (size_t)n + 2 * (size_t)ny) * 8);
+  int rc;
   if (nsub <= 1) {
-    const int rc = integ_noise_cols(ctx, K, n, n, dy, ldy, k1, k2, noise, ny, 0, 1, Iout, var);
-    return rc;
+    rc = integ_noise_cols(ctx, K, n, n, dy, ldy, k1, k2, noise, ny, 0, 1, Iout, var);
+  } else {
+    GPR_TRY(ensure_children(ctx, nsub));
+    rc = run_children(ctx, nsub, [&](gpr_ctx* c, int t) {
+      return integ_noise_cols(c, K, n, n, dy, ldy, k1, k2, noise, ny, t, nsub, Iout, var);
+    });
   }
-  GPR_TRY(ensure_children(ctx, nsub));
-  return run_children(ctx, nsub, [&](gpr_ctx* c, int t) {
-    return integ_noise_cols(c, K, n, n, dy, ldy, k1, k2, noise, ny, t, nsub, Iout, var);
-  });
+  if (rc > 0 && fallback) {  // K + s I not numerically positive definite: the eigensolver
+    ctx->err.clear();
+    return integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, false);
+  }
+  return rc;
 }
 
 int gpr_split_factors(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,

@@ -121,9 +121,14 @@ def test_inverse_diagonal_update_oracle(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("quad", ["auto", "1"])
 @pytest.mark.parametrize("name,dim,n,ne", [("SE", 2, 150, 7), ("SE+WN", 3, 300, 12),
                                            ("SE", 4, 1100, 5)])
-def test_integrate_sample_noise_vs_oracle(name, dim, n, ne):
+def test_integrate_sample_noise_vs_oracle(name, dim, n, ne, quad, monkeypatch):
+    """Positive shifts: the default picks the per-column factorisations at these ne (fewer
+    columns than one eigendecomposition costs); GPR_QUAD_EIGEN=1 forces the eigensolver."""
+    if quad != "auto":
+        monkeypatch.setenv("GPR_QUAD_EIGEN", quad)
     kinds = [O.SE] if name == "SE" else [O.SE, O.WN]
     cov = G.SquaredExp() if name == "SE" else G.SquaredExp() + G.WhiteNoise()
     rng = np.random.default_rng(dim + n)
@@ -211,3 +216,26 @@ def test_integrate_inverse_perturbation_reference(dim, n, ne):
     np.testing.assert_allclose(mu, mu_ex, rtol=1e-5)
     assert np.linalg.norm(S - S_ex) <= 1e-5 * max(np.linalg.norm(S), np.linalg.norm(S_ex))
     np.testing.assert_allclose(S, S_ex, rtol=1e-5, atol=64 * np.finfo(float).eps * k2)
+
+
+@pytest.mark.gpu
+def test_integrate_auto_falls_back_to_eigen_when_not_posdef(monkeypatch):
+    """Nonnegative shifts on a singular K (every point the same, no jitter: K = sigma^2 1 1^T,
+    the second pivot exactly 0): the default's per-column factorisation fails and hands the
+    call to the eigensolver -- no PosDefException, the eigensolver's own result bit for bit."""
+    dim, n, ne = 2, 256, 4
+    rng = np.random.default_rng(21)
+    x = np.full((dim, n), 0.3)
+    Y = rng.random((n, ne))
+    hp = O.default_hp([O.SE], dim, length=2.0)
+    md = G.GPRModel(G.SquaredExp(), hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    noise = np.zeros(ne)
+    I, v = G.integrate(md, a, b, sample_noise=noise, eps=0.0)
+    monkeypatch.setenv("GPR_QUAD_EIGEN", "1")
+    I1, v1 = G.integrate(md, a, b, sample_noise=noise, eps=0.0)
+    np.testing.assert_array_equal(I, I1)
+    np.testing.assert_array_equal(v, v1)
+    monkeypatch.setenv("GPR_QUAD_EIGEN", "0")
+    with pytest.raises(G.PosDefException):
+        G.integrate(md, a, b, sample_noise=noise, eps=0.0)

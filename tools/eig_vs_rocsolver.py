@@ -1,7 +1,7 @@
 """Time the sample_noise quadrature (gpr_integrate_noise: one eigendecomposition of K, then
 (lambda + noise_j)^-1 per column) with the native block-Jacobi eigensolver (default) against
 the rocSOLVER dsyevd comparator (GPR_QUAD_EIGEN=2) and the per-column factorisations
-(GPR_QUAD_EIGEN=0).  GPR_QUAD_EIGEN is read once per process, so run one process per mode:
+(GPR_QUAD_EIGEN=0) and the default choice between them (unset: "auto").  One process per mode:
     GPR_QUAD_EIGEN=2 python tools/eig_vs_rocsolver.py
 Prints one line per size: best of 3 after a warm-up, and the result's max relative difference
 to the default path's saved output (when present).  Not a test and not the product path.
@@ -19,7 +19,7 @@ import gpr_amd as G  # noqa: E402
 
 
 def main():
-    mode = os.environ.get("GPR_QUAD_EIGEN", "1")
+    mode = os.environ.get("GPR_QUAD_EIGEN", "auto")
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
     for n, ne in ((512, 64), (1100, 100), (2048, 128), (4096, 128)):

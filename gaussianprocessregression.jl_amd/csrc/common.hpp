@@ -83,7 +83,7 @@ struct gpr_ctx {
   long long dag_spin_limit = 1ll << 25;  // DAG dependency wait bound in polls (~4 s); the
                                         // GPR_DAG_SPIN_LIMIT environment variable overrides
                                         // it per launch (tests force timeouts with it)
-  int dag_zlag = 2;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
+  int dag_zlag = 4;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
   int dag_rlag = 0;       // other right-hand-side rows after A's row i + lag (GPR_DAG_RLAG;
                           // 1, 2, 4 measured no faster for C2 / C3)
   int dag_fearly = 0;     // diagonal tasks right behind the tile they wait for (GPR_DAG_FEARLY;

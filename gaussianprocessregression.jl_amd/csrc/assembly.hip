@@ -1029,11 +1029,31 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
   double* A = ctx->dgA;
   double* nrmA = A + opA;
   double* B = nrmA + nA;
+  static const int wgs = getenv("GPR_KBUILD_UWGS") ? atoi(getenv("GPR_KBUILD_UWGS")) : 8;
+  static const bool xcd = getenv("GPR_KBUILD_XCD") ? atoi(getenv("GPR_KBUILD_XCD")) != 0 : true;
   if (ctx->kup_items_n != 2 * n + full) {  // work list: strip-major (bj << 16 | segment)
     std::vector<int> items;
     for (int bj = 0; bj * KU_W < n; ++bj) {
       const int rows = full ? n : kup_rows(bj * KU_W, n);
       for (int sg = 0; sg * KU_SEG < rows; ++sg) items.push_back((bj << 16) | sg);
+    }
+    if (xcd) {
+      // XCD-aware order: wave w of workgroup b takes items t = 4 b + w (mod 4 grid), and
+      // workgroups b, b + 8, ... share an XCD (its L2).  Give the workgroups of each residue
+      // b mod 8 the segments sg = residue (mod 8), still strip-major: each XCD then reads one
+      // eighth of the row operands (0.6 of 4.7 MB at C3, inside its 4-MB L2) instead of
+      // streaming all of them through it for every strip.  (Placement is a speed hint only:
+      // any order computes the same values.)
+      const int nit = (int)items.size();
+      const int W = 4 * std::max(1, std::min((nit + 3) / 4, 256 * wgs));
+      std::vector<int> q[8];
+      for (int it : items) q[(it & 0xffff) % 8].push_back(it);
+      size_t pos[8] = {};
+      for (int t = 0; t < nit; ++t) {
+        int g = ((t % W) / 4) % 8;
+        for (int k = 0; k < 8 && pos[g] >= q[g].size(); ++k) g = (g + 1) % 8;
+        items[t] = q[g][pos[g]++];
+      }
     }
     if (ctx->kup_items) {
       HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1055,7 +1075,6 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
     gram_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(xs, n, d, S, nbA, NSE, ctx->dgc, 1.0, B, nullptr);
   }
   LAUNCH_CHECK(ctx);
-  static const int wgs = getenv("GPR_KBUILD_UWGS") ? atoi(getenv("GPR_KBUILD_UWGS")) : 8;
   const int grid = std::max(1, std::min((ctx->kup_nitems + 3) / 4, 256 * wgs));
   kmat_symu_kernel<S, NSE><<<grid, 256, sizeof(double) * (256 + 4 * KU_W) * NSE, ctx->stream>>>(
       kp, A, B, nrmA, nbA, n, K, (size_t)ldk, ctx->kup_items, ctx->kup_nitems, full);

@@ -25,6 +25,7 @@ struct KParams {
   double sigma[KMAXP];           // sigma of each SE part
   int hp_off[KMAXP];             // flat hp index of each SE part's sigma
   double l[KMAXP][KMAXD];        // inverse length-scales (multipliers) per SE part
+  double l2[KMAXP][KMAXD];       // their squares (the gradient pass's distance)
   const double* exptab;          // device table 2^(j/256), j < 256 (ctx->dexptab)
 };
 

@@ -99,7 +99,10 @@ int make_kparams(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d
       if (kp->nse >= KMAXP) return set_err(ctx, GPR_E_UNSUP, "more than %d SquaredExp parts", KMAXP);
       kp->sigma[kp->nse] = hp[off];
       kp->hp_off[kp->nse] = off;
-      for (int k = 0; k < d; ++k) kp->l[kp->nse][k] = hp[off + 1 + k];
+      for (int k = 0; k < d; ++k) {
+        kp->l[kp->nse][k] = hp[off + 1 + k];
+        kp->l2[kp->nse][k] = hp[off + 1 + k] * hp[off + 1 + k];
+      }
       kp->nse++;
       off += d + 1;
     } else if (kinds[i] == GPR_WN) {

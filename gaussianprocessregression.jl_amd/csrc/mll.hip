@@ -88,9 +88,6 @@ __global__ __launch_bounds__(256) void mll_grad_tiles_kernel(KParams kp, const d
 
   int slot = 0;
   for (int p = 0; p < kp.nse; ++p) {
-    double xsr[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) xsr[k] = xr[k] * kp.l[p][(EXACT || k < d) ? k : 0];
     const double* ts = tabs[p];
     double acc_s = 0.0;
     double acc_l[D];
@@ -98,21 +95,31 @@ __global__ __launch_bounds__(256) void mll_grad_tiles_kernel(KParams kp, const d
     for (int k = 0; k < D; ++k) acc_l[k] = 0.0;
     // (not unrolled: unrolled, the wave-uniform point loads of all 16 columns were hoisted
     // into SGPRs and spilled)
+    // K^-1's entries one column ahead (a global load's latency behind the current column's
+    // distance and exponential instead of in front of its weight)
+    const size_t irc = (size_t)min(i, n - 1);
+    double kin = Kinv[irc + (size_t)min(j0 + wv, n - 1) * ldk];
 #pragma unroll 1
     for (int c = 0; c < 16; ++c) {
       const int jr = j0 + wv + 4 * c;
       const int j = min(jr, n - 1);  // wave-uniform: scalar loads of the point
+      const double kcur = kin;
+      if (c < 15) kin = Kinv[irc + (size_t)min(jr + 4, n - 1) * ldk];
       // M_ab = w (alpha_a alpha_b - Kinv_ab), 0 past n
-      const double mv = (irow && jr < n) ? wgt * (ai * alpha[j] - Kinv[(size_t)min(i, n - 1) + (size_t)j * ldk]) : 0.0;
+      const double mv = (irow && jr < n) ? wgt * (ai * alpha[j] - kcur) : 0.0;
       const double* xc = X + (size_t)j * d;
-      double dist = 0.0;
+      // D = sum_k l_k^2 r_k^2 over the raw differences r_k (l_k^2 from the kernel arguments,
+      // four partial sums: no 16-long dependent chain, no scaled copy of the row point held
+      // in registers); dK/dl_k's r_k^2 recomputed after the exponential
+      double dpart[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         if (EXACT || k < d) {
-          const double t = xsr[k] - xc[k] * kp.l[p][k];
-          dist = fma(t, t, dist);
+          const double r = xr[k] - xc[k];
+          dpart[k & 3] = fma(kp.l2[p][k], r * r, dpart[k & 3]);
         }
       }
+      const double dist = (dpart[0] + dpart[1]) + (dpart[2] + dpart[3]);
       const double Kp = kexp_s2(dist, ts) + (i == j ? kp.eps : 0.0);
       const double mk = mv * Kp;
       acc_s += mk;

@@ -181,6 +181,8 @@ struct gpr_ctx {
   int kup_items_n = -1, kup_nitems = 0;
   const double* kup_ptr = nullptr;
   int kup_n = 0, kup_ld = 0;
+  double* dagb = nullptr;       // batched tile-DAG workspace (W slots, task lists, counters)
+  size_t dagb_cap = 0;
   double* deig = nullptr;       // block-Jacobi eigensolver workspace (eigen.hip)
   size_t eig_cap = 0;
   int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)
@@ -301,6 +303,8 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
 // other shapes on a padded copy); dag_shape_ok: the launch takes the shape directly
 bool dag_takes_whole(const gpr_ctx* ctx, int n, int lda, const double* dA);
 bool dag_shape_ok(int n, int lda, const double* dA);
+int launch_potrf_dag_batch(gpr_ctx* ctx, double* dA, size_t strA, int n, int lda, double* dB,
+                           size_t strB, int nrhs, int ldb, int nbatch, int* info_out);
 int launch_potrf_dag_padded(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int nrhs,
                             int ldb);
 int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info,

@@ -147,6 +147,12 @@ struct DagArgs {
   int gbase;
   long long spin_limit;  // polls before a wait gives up (~4 s at 2^25; GPR_DAG_SPIN_LIMIT, tests)
   int mirror;  // DAG_MIRROR: off-diagonal tasks store their loaded A_ij, transposed, at (j, i)
+  // batched launches (launch_potrf_dag_batch): task t belongs to matrix tbatch[t], whose A, B,
+  // W slots, progress counters and info word sit at these strides from the base pointers (the
+  // ticket stays a.sync[0])
+  const int* tbatch;
+  size_t strA, strB, strW;
+  int strS;
 };
 
 __device__ __forceinline__ int ld_sc1(const int* p) {
@@ -441,8 +447,9 @@ __device__ __forceinline__ void dag_gram_task(const DagArgs& a, int i_, int j_,
       }
 }
 
-template <bool GRAM>
-__global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
+template <bool GRAM, bool BATCH>
+__global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a0) {
+  DagArgs a = a0;  // (BATCH: re-pointed at each task's matrix)
   // ONE LDS variable: with separate __shared__ scalars the accesses get alias scopes, and
   // the waitcnt pass then made every fragment read wait for ALL in-flight LDS-DMA (an
   // s_waitcnt vmcnt(0) per stage: the DMA never ran ahead; accumulation at 0.23 instead of
@@ -468,10 +475,15 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
 #endif
   for (;;) {
     if (w == 0) {  // one ticket: lane 0 adds 1, the other lanes 0 (a wave-wide atomic)
-      const int tk = atomicAdd(&a.sync[0], lane == 0 ? 1 : 0);
+      const int tk = atomicAdd(&a0.sync[0], lane == 0 ? 1 : 0);
       const int tk0 = __builtin_amdgcn_readlane(tk, 0);
       s_task = tk0;
-      s_skip = __builtin_amdgcn_readfirstlane(ld_sc1(a.info)) != 0;
+      if (!BATCH) {
+        s_skip = __builtin_amdgcn_readfirstlane(ld_sc1(a.info)) != 0;
+      } else if (tk0 < a0.ntasks) {
+        const int b = __builtin_amdgcn_readfirstlane(a0.tbatch[tk0]);
+        s_skip = __builtin_amdgcn_readfirstlane(ld_sc1(a0.info + b)) != 0;
+      }
     }
     __syncthreads();
     // wave-uniform (SGPR) copies: the loop exit and every branch around the barriers below
@@ -482,6 +494,15 @@ __global__ __launch_bounds__(256, 1) void potrf_dag_kernel(DagArgs a) {
     DTRACE(0, t);
     DTRACE(1, 1);
     if (t >= a.ntasks) break;
+    if (BATCH) {
+      const int b = __builtin_amdgcn_readfirstlane(a0.tbatch[t]);
+      a.A = a0.A + (size_t)b * a0.strA;
+      a.B = a0.B + (size_t)b * a0.strB;
+      a.winv = a0.winv + (size_t)b * a0.strW;
+      a.info = a0.info + b;
+      colprog = a0.sync + (size_t)b * a0.strS + 2;
+      rhsprog = colprog + a.nt;
+    }
     const unsigned code = __builtin_amdgcn_readfirstlane(a.tasks[t]);  // (a vector load)
     if (GRAM && t >= a.gbase) {
       // G_ij = sum_{k >= j} B_ki^T B_kj (i <= j; B lower triangular, so row blocks k < j
@@ -888,9 +909,9 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
     ctx->ls = st;  // TimerScope records on ctx->ls
     TimerScope ts(ctx, solve ? TC_DAG_SOLVE : TC_DAG, flops);  // (solve-only launches apart)
     if (gram)
-      potrf_dag_kernel<true><<<grid, 256, 0, st>>>(a);
+      potrf_dag_kernel<true, false><<<grid, 256, 0, st>>>(a);
     else
-      potrf_dag_kernel<false><<<grid, 256, 0, st>>>(a);
+      potrf_dag_kernel<false, false><<<grid, 256, 0, st>>>(a);
     ctx->ls = ls;
     const hipError_t le = hipGetLastError();
     if (le != hipSuccess) {
@@ -901,6 +922,101 @@ int launch_potrf_dag(gpr_ctx* ctx, double* dA, int n, int lda, double* dB, int n
   if (hook) {
     hook(ctx->dag_hook_user, dA, n, lda, ctx->dag_sync + 2, a.ustored, nt, hook_ev);
     if (hook_ev) hipEventDestroy(hook_ev);
+  }
+  return 0;
+}
+
+// nbatch independent factorisations A_b = U_b^T U_b (A_b = dA + b strA, n x n, ld lda) and
+// B_b <- U_b^{-T} B_b (dB + b strB, n x nrhs, ld ldb; optional) in ONE persistent launch: the
+// tasks of every matrix in one ticket list, row by row across the matrices (row i of each A_b,
+// then row i of each B_b), so the independent chains fill the CUs that one chain leaves idle
+// (a per-matrix launch of a small N is chain-bound).  Per-matrix W slots, progress counters and
+// info words in ctx->dagb; info_out[b] (host) = matrix b's LAPACK info.  The shape conditions
+// are the single launch's (n % 16, 128-B aligned tiles: strides multiples of 16 doubles).
+// Returns 1 when they do not hold (nothing launched), 0 after the launch has completed.
+int launch_potrf_dag_batch(gpr_ctx* ctx, double* dA, size_t strA, int n, int lda, double* dB,
+                           size_t strB, int nrhs, int ldb, int nbatch, int* info_out) {
+  hipStream_t st = ctx->stream;
+  if (nbatch <= 0) return 0;
+  if (ctx->nb != DT || n <= 0 || n % 16 || lda % 16 || strA % 16 || ((uintptr_t)dA & 127) ||
+      n > DT * 32767)
+    return 1;
+  if (dB && (nrhs <= 0 || ldb % 16 || strB % 16 || ((uintptr_t)dB & 127) || nrhs > DT * 65535))
+    return 1;
+  const int nt = (n + DT - 1) / DT, ntr = dB ? (nrhs + DT - 1) / DT : 0;
+  std::vector<unsigned> tasks;
+  std::vector<int> tb;
+  const size_t per = (size_t)nt * (nt + 1) / 2 + (size_t)nt * ntr;
+  tasks.reserve(per * nbatch);
+  tb.reserve(per * nbatch);
+  for (int i = 0; i < nt; ++i) {
+    for (int b = 0; b < nbatch; ++b)
+      for (int j = i; j < nt; ++j) {
+        tasks.push_back(((unsigned)i << 16) | (unsigned)j);
+        tb.push_back(b);
+      }
+    for (int b = 0; b < nbatch; ++b)
+      for (int c = 0; c < ntr; ++c) {
+        tasks.push_back(0x80000000u | ((unsigned)i << 16) | (unsigned)c);
+        tb.push_back(b);
+      }
+  }
+  const int ntasks = (int)tasks.size();
+  const int strS = 2 + nt + ntr;
+  // workspace (doubles): W slots | tasks | tbatch | sync | info (ints packed two per double)
+  const size_t nW = (size_t)nbatch * nt * DT * DT;
+  const size_t nI = (size_t)ntasks * 2 + (size_t)nbatch * strS + (size_t)nbatch;
+  GPR_TRY(ensure_buf(ctx, &ctx->dagb, &ctx->dagb_cap, nW + (nI + 1) / 2 + 1));
+  double* W = ctx->dagb;
+  unsigned* dtasks = reinterpret_cast<unsigned*>(W + nW);
+  int* dtb = reinterpret_cast<int*>(dtasks + ntasks);
+  int* dsync = dtb + ntasks;
+  int* dinfo = dsync + (size_t)nbatch * strS;
+  HIP_TRY(ctx, hipMemcpyAsync(dtasks, tasks.data(), sizeof(unsigned) * ntasks, hipMemcpyHostToDevice, st));
+  HIP_TRY(ctx, hipMemcpyAsync(dtb, tb.data(), sizeof(int) * ntasks, hipMemcpyHostToDevice, st));
+  HIP_TRY(ctx, hipMemsetAsync(dsync, 0, sizeof(int) * ((size_t)nbatch * strS + nbatch), st));
+  if (ctx->ncu <= 0) {
+    hipDeviceProp_t prop;
+    HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
+    ctx->ncu = prop.multiProcessorCount;
+  }
+  DagArgs a{};
+  a.A = dA;
+  a.lda = (size_t)lda;
+  a.n = n;
+  a.nt = nt;
+  a.B = dB;
+  a.ldb = (size_t)(dB ? ldb : 0);
+  a.nrhs = dB ? nrhs : 0;
+  a.ntr = ntr;
+  a.winv = W;
+  a.kglob = 0;
+  a.info = dinfo;
+  a.sync = dsync;
+  a.tasks = dtasks;
+  a.ntasks = ntasks;
+  a.gbase = ntasks;
+  const char* sl = getenv("GPR_DAG_SPIN_LIMIT");
+  a.spin_limit = sl ? std::max(1ll, atoll(sl)) : ctx->dag_spin_limit;
+  a.tbatch = dtb;
+  a.strA = strA;
+  a.strB = strB;
+  a.strW = (size_t)nt * DT * DT;
+  a.strS = strS;
+  const int grid = std::min(ntasks, std::max(1, ctx->ncu));
+  const double flops = nbatch * ((double)n * n * n / 3.0 + (double)n * n * (dB ? nrhs : 0));
+  {
+    TimerScope ts(ctx, TC_DAG, flops);
+    potrf_dag_kernel<false, true><<<grid, 256, 0, st>>>(a);
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return set_err(ctx, GPR_E_HIP, "batched tile-DAG launch: %s", hipGetErrorString(le));
+  }
+  std::vector<int> h(nbatch);
+  HIP_TRY(ctx, hipMemcpyAsync(h.data(), dinfo, sizeof(int) * nbatch, hipMemcpyDeviceToHost, st));
+  HIP_TRY(ctx, hipStreamSynchronize(st));
+  for (int b = 0; b < nbatch; ++b) {
+    if (h[b] < 0) return set_err(ctx, GPR_E_HIP, "batched tile-DAG: a dependency wait timed out");
+    if (info_out) info_out[b] = h[b];
   }
   return 0;
 }

@@ -273,6 +273,7 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dgc) hipFree(ctx->dgc);
   if (ctx->kup_items) hipFree(ctx->kup_items);
   if (ctx->deig) hipFree(ctx->deig);
+  if (ctx->dagb) hipFree(ctx->dagb);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;
   return 0;

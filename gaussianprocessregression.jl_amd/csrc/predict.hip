@@ -705,6 +705,108 @@ static int integ_noise_cols(gpr_ctx* c, const double* K, int ldk, int n, const d
   return 0;
 }
 
+// Batched form of the per-column path: matrices K + noise_b I for a chunk of columns, each
+// padded to n2 = n rounded up to 16 with the identity ([[K + s I, 0], [0, I]] has the factor
+// [[U, 0], [0, I]]), only the upper triangle written (the tile-DAG reads nothing else), and
+// right-hand sides [y_b | k1] (zero-padded) -- one batched tile-DAG launch factors all of them
+// and solves V_b = U_b^{-T} [y_b | k1]; then Iout_b = V_b[:,1] . V_b[:,0] (= k1' (K + s I)^{-1}
+// y_b) and var_b = k2 - ||V_b[:,1]||^2.
+__global__ void quad_batch_prep_kernel(const double* __restrict__ K, int n, int n2,
+                                       const double* __restrict__ noise, const double* __restrict__ dy,
+                                       int ldy, const double* __restrict__ k1, double* __restrict__ W,
+                                       double* __restrict__ Bm, int nb) {
+  const size_t per = (size_t)n2 * n2, tot = per * nb;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += stride) {
+    const int b = (int)(e / per);
+    const size_t rem = e - (size_t)b * per;
+    const int r = (int)(rem % n2), c = (int)(rem / n2);
+    if (r > c) continue;  // (the strict lower triangle is never read)
+    W[e] = (c < n) ? K[(size_t)r + (size_t)c * n] + (r == c ? noise[b] : 0.0) : (r == c ? 1.0 : 0.0);
+  }
+  const size_t totb = (size_t)2 * n2 * nb;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < totb; e += stride) {
+    const int b = (int)(e / (2 * (size_t)n2));
+    const size_t rem = e - (size_t)b * 2 * n2;
+    const int r = (int)(rem % n2), c = (int)(rem / n2);
+    Bm[e] = r < n ? (c == 0 ? dy[(size_t)b * ldy + r] : k1[r]) : 0.0;
+  }
+}
+
+__global__ void quad_batch_reduce_kernel(const double* __restrict__ Bm, int n2, double k2,
+                                         double* __restrict__ out) {
+  const double* V = Bm + (size_t)blockIdx.x * 2 * n2;
+  double sv = 0.0, sk = 0.0;
+  for (int i = threadIdx.x; i < n2; i += 256) {
+    const double a = V[i], c = V[n2 + i];
+    sv = fma(a, c, sv);
+    sk = fma(c, c, sk);
+  }
+  __shared__ double red[2][256];
+  red[0][threadIdx.x] = sv;
+  red[1][threadIdx.x] = sk;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = red[0][0];
+    out[2 * blockIdx.x + 1] = k2 - red[1][0];
+  }
+}
+
+// Returns 0 (done), > 0 the first failing column's info (K + noise_j I not positive
+// definite), 1 with *declined set when the batched launch cannot take the shape.
+static int integ_noise_batched(gpr_ctx* ctx, const double* K, int n, const double* dy, int ldy,
+                               const double* k1, double k2, const double* noise, int ny,
+                               double* Iout, double* var, bool* declined) {
+  *declined = false;
+  const int n2 = (n + 15) / 16 * 16;
+  const size_t per = (size_t)n2 * n2 + 2 * (size_t)n2;
+  static const double budget = getenv("GPR_QUAD_BATCH_GB") ? atof(getenv("GPR_QUAD_BATCH_GB")) : 16.0;
+  const int nbc = (int)std::max<size_t>(1, std::min<size_t>((size_t)ny, (size_t)(budget * 1e9 / 8.0) / per));
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per * nbc + (size_t)3 * nbc + 16));
+  double* W = ctx->dbig;
+  double* Bm = W + (size_t)n2 * n2 * nbc;
+  double* dnoise = Bm + (size_t)2 * n2 * nbc;
+  double* out = dnoise + nbc;
+  std::vector<int> info(nbc);
+  std::vector<double> h(2 * (size_t)nbc);
+  for (int j0 = 0; j0 < ny; j0 += nbc) {
+    const int nb = std::min(nbc, ny - j0);
+    HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise + j0, sizeof(double) * nb, hipMemcpyHostToDevice,
+                                ctx->stream));
+    const size_t tot = (size_t)n2 * n2 * nb;
+    const int blocks = (int)std::min<size_t>((tot + 255) / 256, 8192);
+    quad_batch_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(K, n, n2, dnoise, dy + (size_t)j0 * ldy,
+                                                            ldy, k1, W, Bm, nb);
+    LAUNCH_CHECK(ctx);
+    const int rc = launch_potrf_dag_batch(ctx, W, (size_t)n2 * n2, n2, n2, Bm, (size_t)2 * n2, 2, n2,
+                                          nb, info.data());
+    if (rc == 1) {
+      *declined = true;
+      return 1;
+    }
+    if (rc) return rc;
+    for (int b = 0; b < nb; ++b)
+      if (info[b] > 0) return info[b];
+    quad_batch_reduce_kernel<<<nb, 256, 0, ctx->stream>>>(Bm, n2, k2, out);
+    LAUNCH_CHECK(ctx);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), out, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int b = 0; b < nb; ++b) {
+      Iout[j0 + b] = h[2 * b];
+      var[j0 + b] = h[2 * b + 1];
+    }
+  }
+  return 0;
+}
+
 // ---- rocSOLVER, dlopen'd (the process's own librocsolver.so.0 if loaded -- torch carries
 // one -- else the system's; no link-time dependency), for the eigendecomposition of K
 struct RocsolverApi {
@@ -891,23 +993,36 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   // Jacobi eigensolver.  GPR_QUAD_EIGEN=0: K + noise_j I factored per column (PD shifts only);
   // =2: rocSOLVER's dsyevd for the decomposition (timing comparator; falls back to the
   // per-column factorisations when it cannot be loaded)
-  // Unset: per-column factorisations when every shift is nonnegative (K + s I is then positive
-  // definite) and ny of them cost less than one eigendecomposition (measured crossover,
-  // profiles/r04_eig_speed.txt: ~ny < n / 8 + 64), else the eigensolver; a per-column path that
-  // meets a non-positive-definite K + s I falls back to the eigensolver.  =1 forces the
-  // eigensolver.
+  // Unset: per-column factorisations -- batched, one tile-DAG launch -- when every shift is
+  // nonnegative (K + s I is then positive definite) and ny of them cost less than one
+  // eigendecomposition (profiles/r04_eig_speed.txt: ny <= n / 2 + 512 is conservative), else
+  // the eigensolver; a per-column path that meets a non-positive-definite K + s I falls back to
+  // the eigensolver.  =1 forces the eigensolver, =0 the factorisations (GPR_QUAD_SEQ: one at a
+  // time, as before the batched launch).
   const char* qe = getenv("GPR_QUAD_EIGEN");
   int qmode = qe ? atoi(qe) : -1;
   bool fallback = false;
   if (qmode < 0) {
     double smin = noise[0];
     for (int j = 1; j < ny; ++j) smin = std::min(smin, noise[j]);
-    qmode = (smin >= 0.0 && ny < n / 8 + 64) ? 0 : 1;
+    qmode = (smin >= 0.0 && ny <= n / 2 + 512) ? 0 : 1;
     fallback = qmode == 0;
   }
   if (qmode != 0) {
     const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode == 2);
     if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
+  }
+  if (!getenv("GPR_QUAD_SEQ")) {  // the batched launch (GPR_QUAD_SEQ: one column at a time)
+    bool declined = false;
+    const int rc = integ_noise_batched(ctx, K, n, dy, ldy, k1, k2, noise, ny, Iout, var, &declined);
+    if (!declined) {
+      if (rc > 0 && fallback) {  // K + s I not numerically positive definite: the eigensolver
+        ctx->err.clear();
+        return integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, false);
+      }
+      return rc;
+    }
+    ctx->err.clear();
   }
   int nsub = std::min(std::min(ctx->cv_streams, (int)gpr_ctx::CV_MAX_SUB), ny);
   if (n > 8192) nsub = 1;

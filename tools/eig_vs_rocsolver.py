@@ -43,7 +43,7 @@ def main():
             r = np.load(ref)
             got = np.r_[mu, S]
             diff = f"  max rel diff vs native {np.max(np.abs(got - r) / np.abs(r)):.2e}"
-        print(f"GPR_QUAD_EIGEN={mode} n={n:5d} ne={ne:4d}: {best * 1e3:9.1f} ms{diff}", flush=True)
+        print(f"GPR_QUAD_EIGEN={mode}{' SEQ' if os.environ.get('GPR_QUAD_SEQ') else ''} n={n:5d} ne={ne:4d}: {best * 1e3:9.1f} ms{diff}", flush=True)
 
 
 if __name__ == "__main__":

@@ -627,6 +627,131 @@ static int cv_folds(gpr_ctx* c, const int* kinds, int nk, const double* hp, int 
   return 0;
 }
 
+// A[c + c lda] = 1 for n <= c < n2 and zeros above it (the upper triangle of [[A, 0], [0, I]]),
+// for nb matrices at stride sA
+__global__ void pad_identity_kernel(double* __restrict__ A, size_t lda, size_t sA, int n, int n2,
+                                    int nb) {
+  const size_t per = (size_t)n2 * (n2 - n), tot = per * nb;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / per);
+    const size_t rem = e - (size_t)b * per;
+    const int r = (int)(rem % n2), c = n + (int)(rem / n2);
+    if (r <= c) A[(size_t)b * sA + r + (size_t)c * lda] = r == c ? 1.0 : 0.0;
+  }
+}
+
+// gpr_cv_batch with every fold's factorisation in ONE batched tile-DAG launch (and, for
+// Mahalanobis, every fold's Sigma_p factorisation in a second): per fold K_f (padded to n2, a
+// multiple of 16, with the identity), W_f = [K(x_tr, x_ts) | y_tr] (zero-padded rows), the prior
+// Sigma_f = K(x_ts, x_ts) (padded to s2); the launch leaves V_f = U_f^{-T} W_f, then mu =
+// V_kx^T v_y, Sigma_p = Sigma_f - V_kx^T V_kx (upper triangle), and the loss -- gpr_fit_predict's
+// FULL path per fold with its chain-bound factorisations batched ("cv needs batched
+// small POTRFs").  Returns > 0 as the sequential path does (a fold's info), 0 when done.
+static int cv_folds_batched(gpr_ctx* ctx, const KParams& kp, int d, const double* dX, int n,
+                            const double* dy, const int* trn, int ntrn, const int* tst, int ntst,
+                            int nfold, int cost, double* lss) {
+  const int n2 = (ntrn + 15) / 16 * 16, s2 = (ntst + 15) / 16 * 16;
+  const size_t szK = (size_t)n2 * n2, szW = (size_t)n2 * (ntst + 1), szS = (size_t)s2 * s2;
+  const size_t per = szK + szW + szS + 2 * (size_t)s2 + 1;
+  const double budget = getenv("GPR_CV_BATCH_GB") ? atof(getenv("GPR_CV_BATCH_GB")) : 16.0;
+  const int nfc = (int)std::max<size_t>(1, std::min<size_t>((size_t)nfold, (size_t)(budget * 1e9 / 8.0) / per));
+  const size_t scratch = (size_t)d * (ntrn + ntst) + ntrn;
+  const size_t nidx = (size_t)nfc * (ntrn + ntst);
+  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per * nfc + scratch + (nidx + 1) / 2 + 16));
+  double* Kb = ctx->dbig;                 // nfc x szK
+  double* Wb = Kb + szK * nfc;            // nfc x szW
+  double* Sb = Wb + szW * nfc;            // nfc x szS
+  double* Yp = Sb + szS * nfc;            // nfc x s2: mu, then delta / U^{-T} delta
+  double* Yt = Yp + (size_t)s2 * nfc;     // nfc x s2: y_ts
+  double* dl = Yt + (size_t)s2 * nfc;     // nfc
+  double* xtr = dl + nfc;
+  double* xts = xtr + (size_t)d * ntrn;
+  double* ytr = xts + (size_t)d * ntst;
+  int* di = reinterpret_cast<int*>(ytr + ntrn);
+  std::vector<int> hidx(nidx), info(nfc);
+  std::vector<double> hl(nfc);
+  hipStream_t st = ctx->stream;
+  for (int f0 = 0; f0 < nfold; f0 += nfc) {
+    const int nb = std::min(nfc, nfold - f0);
+    for (int i = 0; i < nb; ++i) {
+      const size_t f = (size_t)f0 + i;
+      std::copy(trn + f * ntrn, trn + (f + 1) * ntrn, hidx.begin() + (size_t)i * ntrn);
+      std::copy(tst + f * ntst, tst + (f + 1) * ntst, hidx.begin() + (size_t)nb * ntrn + (size_t)i * ntst);
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(di, hidx.data(), (size_t)nb * (ntrn + ntst) * sizeof(int),
+                                hipMemcpyHostToDevice, st));
+    // zero-padded right-hand sides and vectors; the padded matrices' extra columns by the kernel
+    HIP_TRY(ctx, hipMemsetAsync(Wb, 0, sizeof(double) * szW * nb, st));
+    HIP_TRY(ctx, hipMemsetAsync(Yp, 0, sizeof(double) * 2 * (size_t)s2 * nfc, st));
+    for (int i = 0; i < nb; ++i) {
+      const int* itr = di + (size_t)i * ntrn;
+      const int* its = di + (size_t)nb * ntrn + (size_t)i * ntst;
+      double* K = Kb + szK * i;
+      double* W = Wb + szW * i;
+      double* S = Sb + szS * i;
+      cv_gather_kernel<<<std::min((ntrn * (d + 1) + 255) / 256, 1024), 256, 0, st>>>(dX, dy, d, itr,
+                                                                                   ntrn, xtr, ytr);
+      LAUNCH_CHECK(ctx);
+      cv_gather_kernel<<<std::min((ntst * (d + 1) + 255) / 256, 1024), 256, 0, st>>>(
+          dX, dy, d, its, ntst, xts, Yt + (size_t)s2 * i);
+      LAUNCH_CHECK(ctx);
+      GPR_TRY(launch_kernel_matrix(ctx, kp, xtr, ntrn, nullptr, ntrn, 1, K, n2));
+      GPR_TRY(launch_kernel_matrix(ctx, kp, xtr, ntrn, xts, ntst, 0, W, n2));
+      HIP_TRY(ctx, hipMemcpyAsync(W + (size_t)n2 * ntst, ytr, sizeof(double) * ntrn,
+                                  hipMemcpyDeviceToDevice, st));
+      GPR_TRY(launch_kernel_matrix(ctx, kp, xts, ntst, nullptr, ntst, 1, S, s2));
+    }
+    if (n2 > ntrn) {
+      pad_identity_kernel<<<1024, 256, 0, st>>>(Kb, n2, szK, ntrn, n2, nb);
+      LAUNCH_CHECK(ctx);
+    }
+    if (s2 > ntst) {
+      pad_identity_kernel<<<1024, 256, 0, st>>>(Sb, s2, szS, ntst, s2, nb);
+      LAUNCH_CHECK(ctx);
+    }
+    int rc = launch_potrf_dag_batch(ctx, Kb, szK, n2, n2, Wb, szW, ntst + 1, n2, nb, info.data());
+    if (rc) return rc == 1 ? set_err(ctx, GPR_E_HIP, "batched cross-validation: shape declined") : rc;
+    for (int i = 0; i < nb; ++i)
+      if (info[i] > 0) return info[i];
+    for (int i = 0; i < nb; ++i) {
+      const double* W = Wb + szW * i;
+      double* S = Sb + szS * i;
+      double* yp = Yp + (size_t)s2 * i;
+      colgemv_kernel<<<(ntst + 3) / 4, 256, 0, st>>>(W, (size_t)n2, n2, ntst, W + (size_t)n2 * ntst,
+                                                      (size_t)n2, 1, yp, (size_t)ntst);
+      LAUNCH_CHECK(ctx);
+      GemmArgs g{};
+      g.P = W; g.ldp = n2;
+      g.Q = W; g.ldq = n2;
+      g.C = S; g.ldc = s2;
+      g.M = ntst; g.N = ntst; g.K = n2;
+      g.alpha = -1.0; g.beta = 1.0;
+      g.upper = 1;
+      GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+      cv_loss_kernel<<<1, 256, 0, st>>>(Yt + (size_t)s2 * i, yp, S, (size_t)s2, ntst,
+                                        cost == GPR_COST_MAHALANOBIS ? -1 : cost, dl + i);
+      LAUNCH_CHECK(ctx);
+    }
+    if (cost == GPR_COST_MAHALANOBIS) {
+      // delta = y - yp; Sigma_p = U^T U; ||U^{-T} delta||^2 (:25-30) -- the second batch
+      rc = launch_potrf_dag_batch(ctx, Sb, szS, s2, s2, Yp, (size_t)s2, 1, s2, nb, info.data());
+      if (rc) return rc == 1 ? set_err(ctx, GPR_E_HIP, "batched cross-validation: shape declined") : rc;
+      for (int i = 0; i < nb; ++i)
+        if (info[i] > 0) return info[i];
+      for (int i = 0; i < nb; ++i) {
+        cv_loss_kernel<<<1, 256, 0, st>>>(Yt + (size_t)s2 * i, Yp + (size_t)s2 * i, Sb + szS * i,
+                                          (size_t)s2, ntst, 0, dl + i);
+        LAUNCH_CHECK(ctx);
+      }
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(hl.data(), dl, sizeof(double) * nb, hipMemcpyDeviceToHost, st));
+    HIP_TRY(ctx, hipStreamSynchronize(st));
+    for (int i = 0; i < nb; ++i) lss[(size_t)f0 + i] = hl[i];
+  }
+  return 0;
+}
+
 int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                  const double* dX, int n, const double* dy, const int* trn, int ntrn,
                  const int* tst, int ntst, int nfold, int cost, double eps, double* lss) {
@@ -644,6 +769,10 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
       if (tst[f * ntst + j] < 0 || tst[f * ntst + j] >= n)
         return set_err(ctx, GPR_E_ARG, "test index out of range");
   }
+  // Every fold's factorisation in one batched tile-DAG launch (GPR_CV_BATCH=1; else the
+  // per-fold path below, folds spread over child contexts).
+  if (getenv("GPR_CV_BATCH") && atoi(getenv("GPR_CV_BATCH")) != 0)
+    return cv_folds_batched(ctx, kp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, cost, lss);
   // A fold below ~8k training points is a latency-bound chain of small launches (diag
   // block, panel GEMM, update per 128 columns) that leaves most CUs idle, so independent
   // folds run concurrently, one child context (own streams, own workspace) per host thread.
@@ -767,7 +896,7 @@ static int integ_noise_batched(gpr_ctx* ctx, const double* K, int n, const doubl
   *declined = false;
   const int n2 = (n + 15) / 16 * 16;
   const size_t per = (size_t)n2 * n2 + 2 * (size_t)n2;
-  static const double budget = getenv("GPR_QUAD_BATCH_GB") ? atof(getenv("GPR_QUAD_BATCH_GB")) : 16.0;
+  const double budget = getenv("GPR_QUAD_BATCH_GB") ? atof(getenv("GPR_QUAD_BATCH_GB")) : 16.0;
   const int nbc = (int)std::max<size_t>(1, std::min<size_t>((size_t)ny, (size_t)(budget * 1e9 / 8.0) / per));
   GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per * nbc + (size_t)3 * nbc + 16));
   double* W = ctx->dbig;

@@ -239,3 +239,34 @@ def test_integrate_auto_falls_back_to_eigen_when_not_posdef(monkeypatch):
     monkeypatch.setenv("GPR_QUAD_EIGEN", "0")
     with pytest.raises(G.PosDefException):
         G.integrate(md, a, b, sample_noise=noise, eps=0.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ne", [(300, 9), (1040, 6)])
+def test_integrate_batched_columns_chunking_and_sequential(n, ne, monkeypatch):
+    """The default's batched launch (every K + s_j I factored and solved in one tile-DAG
+    launch) is the same computation per column whatever the batch: a 1-column memory budget
+    (GPR_QUAD_BATCH_GB, one launch per column) gives bit for bit the same result; the
+    sequential per-column path (GPR_QUAD_SEQ) and the oracle agree to rounding."""
+    dim = 3
+    kinds = [O.SE, O.WN]
+    rng = np.random.default_rng(n + ne)
+    x = rng.random((dim, n))
+    Y = rng.random((n, ne))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    noise = 1e-3 * (1.0 + rng.random(ne))
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    monkeypatch.setenv("GPR_QUAD_BATCH_GB", "1e-9")
+    I1, v1 = G.integrate(md, a, b, sample_noise=noise)
+    np.testing.assert_array_equal(I, I1)
+    np.testing.assert_array_equal(v, v1)
+    monkeypatch.delenv("GPR_QUAD_BATCH_GB")
+    monkeypatch.setenv("GPR_QUAD_SEQ", "1")
+    Is, vs = G.integrate(md, a, b, sample_noise=noise)
+    np.testing.assert_allclose(Is, I, rtol=1e-10)
+    np.testing.assert_allclose(vs, v, rtol=1e-8, atol=1e-12 * O.antideriv2_se(hp, a, b))
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I, Io, rtol=1e-8)
+    np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))

@@ -1,54 +1,48 @@
-"""Time cv_batch (src/crossval.jl:13-35) on the device: k-fold cross-validation of an SE+WN
-model, Mahalanobis loss (the heaviest: fit + full-covariance posterior + a second POTRF per
-fold).  Prints one JSON line per (n, k): folds/s and ms per fold.
-
-  python tools/bench_cv.py [--sizes 2048:64,8192:819,16384:1638] [--reps 3]
+"""Cross-validation timing (gpr_cv_batch, src/crossval.jl:13-35): every fold's factorisation
+in one batched tile-DAG launch (GPR_CV_BATCH=1) against the per-fold path over child contexts, and the two results' largest relative difference.  Not a test.
+    python tools/bench_cv.py
 """
-import argparse
-import json
 import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gaussianprocessregression.jl_amd"))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
 import gpr_amd as G  # noqa: E402
+from gpr_amd import crossval as CV  # noqa: E402
+
+
+def timed(f, reps=3):
+    f()
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = f()
+        best = min(best, time.perf_counter() - t0)
+    return best, out
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--sizes", default="2048:64,8192:819,16384:1638")
-    ap.add_argument("--d", type=int, default=8)
-    ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--cost", default="Mahalanobis")
-    a = ap.parse_args()
-    cost = {"MSE": G.MSE, "ChiSq": G.ChiSq, "Mahalanobis": G.Mahalanobis}[a.cost]()
-    for spec in a.sizes.split(","):
-        n, k = (int(v) for v in spec.split(":"))
-        rng = np.random.default_rng(0)
-        x = rng.random((a.d, n))
-        y = np.sin(x.sum(axis=0)) ** 2
-        hp = np.array([1.0] + [3.0] * a.d + [0.1])
+    for n, k, d in ((1000, 100, 4), (2000, 200, 8), (4096, 256, 8), (8192, 512, 8)):
+        rng = np.random.default_rng(n)
+        x = rng.random((d, n))
+        y = np.sin(x.sum(0)) ** 2
+        hp = np.r_[1.0, [3.0 * np.sqrt(8.0 / d)] * d, 0.1]
         md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
-        cvset = G.kfoldcv(n, k, rng=np.random.default_rng(1))
-        G.cv_batch(md, cost, x, y, cvset)  # warm-up (allocations, code objects)
-        ts = []
-        for _ in range(a.reps):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            lss = G.cv_batch(md, cost, x, y, cvset)
-            ts.append(time.perf_counter() - t0)
-        t = min(ts)
-        nf = len(cvset[0])
-        print(json.dumps({"bench": "cv_batch", "cost": a.cost, "n": n, "k": k, "d": a.d,
-                          "folds": nf, "ntrn": n - k, "s": round(t, 4),
-                          "ms_per_fold": round(1e3 * t / nf, 3),
-                          "folds_per_s": round(nf / t, 2),
-                          "mean_loss": float(np.mean(lss))}), flush=True)
+        cvset = CV.kfoldcv(n, k, rng=np.random.default_rng(1))
+        for cost in (CV.MSE(), CV.Mahalanobis()):
+            os.environ["GPR_CV_BATCH"] = "1"
+            tb, lb = timed(lambda: CV.cv_batch(md, cost, x, y, cvset))
+            os.environ["GPR_CV_BATCH"] = "0"
+            ts, ls = timed(lambda: CV.cv_batch(md, cost, x, y, cvset))
+            os.environ.pop("GPR_CV_BATCH", None)
+            rel = np.max(np.abs(lb - ls) / np.abs(ls))
+            print(f"n={n:5d} folds={n // k:3d} ntrn={n - k:5d} ntst={k:4d} {type(cost).__name__:11s}: "
+                  f"batched {tb * 1e3:8.1f} ms  per-fold {ts * 1e3:8.1f} ms  max rel diff {rel:.1e}",
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -123,3 +123,27 @@ def test_cv_concurrent_folds_bit_identical(monkeypatch):
         ctx.close()
     np.testing.assert_array_equal(out["1"], out["4"])
     np.testing.assert_array_equal(out["1"], out["8"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cname", ["MSE", "ChiSq", "Mahalanobis"])
+def test_cv_batched_launch_vs_per_fold(cname, monkeypatch):
+    """Every fold's factorisation (and, for Mahalanobis, every Sigma_p's) in one batched tile-DAG
+    launch (GPR_CV_BATCH=1; padded to multiples of 16: ntrn = 341, ntst = 31 here) against the
+    per-fold path: the same losses to rounding; a one-fold memory budget (one launch per fold)
+    gives the batched result bit for bit."""
+    d, n, k = 3, 372, 31
+    x, y = _data(d, n, 8)
+    hp = O.default_hp(["SE", "WN"], d, length=2.0)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cvset = G.kfoldcv(n, k, rng=np.random.default_rng(4))
+    monkeypatch.setenv("GPR_CV_BATCH", "0")
+    seq = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
+    monkeypatch.setenv("GPR_CV_BATCH", "1")
+    bat = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
+    np.testing.assert_allclose(bat, seq, rtol=1e-9, atol=0)
+    monkeypatch.setenv("GPR_CV_BATCH_GB", "1e-9")
+    one = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
+    np.testing.assert_array_equal(one, bat)
+    want = O.cv_batch(["SE", "WN"], hp, cname, x, y, cvset)
+    np.testing.assert_allclose(bat, want, rtol=1e-8, atol=0)

@@ -265,7 +265,7 @@ def test_integrate_batched_columns_chunking_and_sequential(n, ne, monkeypatch):
     monkeypatch.delenv("GPR_QUAD_BATCH_GB")
     monkeypatch.setenv("GPR_QUAD_SEQ", "1")
     Is, vs = G.integrate(md, a, b, sample_noise=noise)
-    np.testing.assert_allclose(Is, I, rtol=1e-10)
+    np.testing.assert_allclose(Is, I, rtol=1e-9)
     np.testing.assert_allclose(vs, v, rtol=1e-8, atol=1e-12 * O.antideriv2_se(hp, a, b))
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
     np.testing.assert_allclose(I, Io, rtol=1e-8)

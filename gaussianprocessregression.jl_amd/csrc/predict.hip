@@ -769,9 +769,9 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
       if (tst[f * ntst + j] < 0 || tst[f * ntst + j] >= n)
         return set_err(ctx, GPR_E_ARG, "test index out of range");
   }
-  // Every fold's factorisation in one batched tile-DAG launch (GPR_CV_BATCH=1; else the
-  // per-fold path below, folds spread over child contexts).
-  if (getenv("GPR_CV_BATCH") && atoi(getenv("GPR_CV_BATCH")) != 0)
+  // Every fold's factorisation in one batched tile-DAG launch (default; GPR_CV_BATCH=0: the
+  // per-fold path below, folds spread over child contexts -- 1.1-2.7x slower, tools/bench_cv.py)
+  if (!getenv("GPR_CV_BATCH") || atoi(getenv("GPR_CV_BATCH")) != 0)
     return cv_folds_batched(ctx, kp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, cost, lss);
   // A fold below ~8k training points is a latency-bound chain of small launches (diag
   // block, panel GEMM, update per 128 columns) that leaves most CUs idle, so independent

@@ -1,6 +1,6 @@
 """Cross-validation timing (gpr_cv_batch, src/crossval.jl:13-35): every fold's factorisation
-in one batched tile-DAG launch (GPR_CV_BATCH=1) against the per-fold path over child
-contexts, and the two results' largest relative difference.  Not a test.
+in one batched tile-DAG launch (default, GPR_CV_BATCH=1) against the per-fold path over
+child contexts (GPR_CV_BATCH=0), and the two results' largest relative difference.  Not a test.
     python tools/bench_cv.py
 """
 import os

@@ -1122,19 +1122,19 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   // Jacobi eigensolver.  GPR_QUAD_EIGEN=0: K + noise_j I factored per column (PD shifts only);
   // =2: rocSOLVER's dsyevd for the decomposition (timing comparator; falls back to the
   // per-column factorisations when it cannot be loaded)
-  // Unset: per-column factorisations -- batched, one tile-DAG launch -- when every shift is
-  // nonnegative (K + s I is then positive definite) and ny of them cost less than one
-  // eigendecomposition (profiles/r04_eig_speed.txt: ny <= n / 2 + 512 is conservative), else
-  // the eigensolver; a per-column path that meets a non-positive-definite K + s I falls back to
-  // the eigensolver.  =1 forces the eigensolver, =0 the factorisations (GPR_QUAD_SEQ: one at a
+  // Unset: per-column factorisations -- batched, one tile-DAG launch -- when ny of them cost
+  // less than one eigendecomposition (profiles/r04_eig_speed.txt: ny <= n / 2 + 512 is
+  // conservative), else the eigensolver; a batch that meets a non-positive-definite K + s I
+  // (a shift at or below -lambda_min(K)) falls back to the eigensolver.  =1 forces the eigensolver, =0 the factorisations (GPR_QUAD_SEQ: one at a
   // time, as before the batched launch).
   const char* qe = getenv("GPR_QUAD_EIGEN");
   int qmode = qe ? atoi(qe) : -1;
   bool fallback = false;
   if (qmode < 0) {
-    double smin = noise[0];
-    for (int j = 1; j < ny; ++j) smin = std::min(smin, noise[j]);
-    qmode = (smin >= 0.0 && ny <= n / 2 + 512) ? 0 : 1;
+    // any shift: K + s I is positive definite for s >= 0 and for -lambda_min(K) < s < 0; a
+    // batch holding an indefinite one fails at that matrix's first non-positive pivot and the
+    // call goes to the eigensolver (a wasted launch of a few ms against the eigensolver's tens)
+    qmode = ny <= n / 2 + 512 ? 0 : 1;
     fallback = qmode == 0;
   }
   if (qmode != 0) {

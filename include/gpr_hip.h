@@ -243,10 +243,11 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  * which never forms P: T = P' [y | k1] is carried through the rotations), then Iout[j] =
  * sum_i T_ij (P'k1)_i / (lambda_i + noise_j) and var[j] = k2 - sum_i (P'k1)_i^2 / (lambda_i +
  * noise_j): any shift, no factorisation, never info > 0 (an indefinite K + noise_j I gives the
- * reference's indefinite solve).  Default: when every noise_j >= 0 and ny <= n/2 + 512, the
- * K + noise_j I are factored instead -- all in one batched tile-DAG launch that also solves
- * U_j^{-T} [y_j | k1] (same result within rounding) -- and a factorisation that fails hands the
- * call to the eigensolver, so the default never returns info > 0 either.  GPR_QUAD_EIGEN=1: always the eigensolver;
+ * reference's indefinite solve).  Default: when ny <= n/2 + 512, the K + noise_j I are
+ * factored instead -- all in one batched tile-DAG launch that also solves U_j^{-T} [y_j | k1]
+ * (same result within rounding) -- and a factorisation that fails (a shift at or below
+ * -lambda_min(K)) hands the call to the eigensolver, so the default never returns info > 0
+ * either.  GPR_QUAD_EIGEN=1: always the eigensolver;
  * =0: always the factorisations (positive definite shifts only; info > 0 -- PosDefException
  * -- for the others); =2: rocSOLVER dsyevd (dlopen'd) for the decomposition -- a timing
  * comparator, not the product path. */

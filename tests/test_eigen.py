@@ -98,9 +98,13 @@ def test_syev_diagonal_and_zero():
     np.testing.assert_allclose(np.abs(C), np.sqrt(0.5), rtol=1e-15)
 
 
-def test_integrate_noise_native_vs_rocsolver_comparator(monkeypatch):
-    """The product path (hand-written eigensolver) against rocSOLVER's dsyevd as a comparator
+@pytest.mark.parametrize("quad", ["1", "auto"])
+def test_integrate_noise_native_vs_rocsolver_comparator(quad, monkeypatch):
+    """The hand-written eigensolver (GPR_QUAD_EIGEN=1) and the default (here the batched
+    factorisations: every shift above -lambda_min) against rocSOLVER's dsyevd as a comparator
     (GPR_QUAD_EIGEN=2, timing/cross-check only) and against the oracle's eigen path."""
+    if quad != "auto":
+        monkeypatch.setenv("GPR_QUAD_EIGEN", quad)
     dim, n, ne = 3, 600, 6
     kinds = [O.SE, O.WN]
     rng = np.random.default_rng(9)

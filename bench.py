@@ -130,8 +130,8 @@ def parse():
     ap.add_argument("--kernel", default="SE+SE+WN")
     ap.add_argument("--nb", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-n", type=int, default=32768)
-    ap.add_argument("--cpu-np", type=int, default=8192)
+    ap.add_argument("--cpu-n", type=int, default=None, help="CPU baseline N (default --n)")
+    ap.add_argument("--cpu-np", type=int, default=None, help="CPU baseline np (default --np)")
     ap.add_argument("--no-split", action="store_true",
                     help="skip the C5 split-predict leg (extra key `split_predict`)")
     ap.add_argument("--split-steps", type=int, default=2)
@@ -139,13 +139,16 @@ def parse():
                     help="skip the C5 leg's full-range variant (var_range = 1:ne, SURVEY 8d's "
                          "throughput configuration: ~17 s per step on one GPU, 1 warm-up + 1 step)")
     ap.add_argument("--split-timeout", type=float, default=420.0,
-                    help="watchdog: end the process (exit 0, headline already printed) if the "
+                    help="watchdog: end the process (exit 3, headline already printed) if the "
                          "C5 leg runs longer than this many seconds")
     # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices by
     # LOCAL_RANK modulo the device count): gloo carries the collectives (RCCL refuses two
     # ranks on one device); the driver's runs use the default nccl (= RCCL), one rank per GPU
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.cpu_n = a.cpu_n or a.n
+    a.cpu_np = a.cpu_np or a.npred
+    return a
 
 
 def kinds_of(name):
@@ -562,7 +565,7 @@ def main():
             print(json.dumps({"split_predict": {"value": None, "error":
                                                 f"timed out after {a.split_timeout:.0f} s"}}),
                   file=sys.stderr, flush=True)
-            os._exit(0)
+            os._exit(3)  # (non-zero: a hung collective must not read as success)
 
         wd = threading.Timer(a.split_timeout, _watchdog)
         wd.daemon = True

@@ -39,7 +39,77 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--d", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-n", type=int, default=4096,
+                    help="bounded CPU sample: the oracle's C4 evaluation at this N, each stage "
+                         "extrapolated to --n by its complexity")
     return ap.parse_args()
+
+
+def cpu_baseline(a, hp):
+    """The CPU oracle (test infrastructure; this leg only) on a bounded sample of the C4
+    evaluation: loss_grad! for an MllGradCache in the reference's order (src/cost.jl:83-126 --
+    K, cholesky!, ldiv!, K^{-1} = ldiv!(kchol, I), the MLL and every dK/dtheta_i's
+    grad(MLL, ...) term, LogScale) at N = a.cpu_n, d = a.d, median of 3 after a warm-up, each
+    stage scaled to N = a.n by its complexity (N^2, N^3, N^2, N^3, N^2).  Threads: the box's CPU
+    share (OMP_NUM_THREADS) for OpenBLAS, reported by threadpoolctl."""
+    import scipy.linalg as sla
+    from threadpoolctl import threadpool_info, threadpool_limits
+
+    sys.path.insert(0, ROOT)
+    from oracle import gpr_oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    n, d = a.cpu_n, a.d
+    kinds = [O.SE, O.WN]
+    x = np.random.default_rng(0).random((d, n))
+    y = np.sin(x.sum(0)) ** 2
+
+    def run():
+        t = [time.perf_counter()]
+        K = O.kernel(kinds, hp, x)
+        t.append(time.perf_counter())
+        U = sla.cholesky(K, lower=False, check_finite=False)
+        t.append(time.perf_counter())
+        alpha = O.cho_solve_upper(U, y)
+        t.append(time.perf_counter())
+        Kinv = O.kinv_from_upper(U)
+        t.append(time.perf_counter())
+        g = np.array([O.mll_grad_term(O.kernel_grad(kinds, i, hp, x), alpha, Kinv)
+                      for i in range(1, len(hp) + 1)]) * hp
+        val = O.mll_value(U, y, alpha)
+        t.append(time.perf_counter())
+        assert np.isfinite(g).all() and np.isfinite(val)
+        return np.diff(t)
+
+    with threadpool_limits(limits=threads):
+        blas = [{"lib": i.get("internal_api"), "version": i.get("version"),
+                 "threads": i.get("num_threads")}
+                for i in threadpool_info() if i.get("user_api") == "blas"
+                and "scipy.libs" in i.get("filepath", "")]
+        run()
+        reps = [run() for _ in range(3)]
+    t = np.median(np.stack(reps), axis=0)
+    r = a.n / n
+    scale = np.array([r ** 2, r ** 3, r ** 2, r ** 3, r ** 2])
+    t_eval = float(np.sum(t * scale))
+    return {
+        "value": 1.0 / t_eval, "unit": "loss_grad! evaluations/s", "cores": threads,
+        "kind": "port", "blas": blas,
+        "measured_config": {"N": n, "d": d, "stage_s": [round(v, 4) for v in t.tolist()]},
+        "sample": (f"oracle (NumPy/SciPy OpenBLAS, {threads} threads) C4 evaluation at N={n}, "
+                   f"d={d} (median of 3 after 1 warm-up): stages [kernel, dpotrf, dpotrs, "
+                   f"K^-1, mll+{len(hp)} grad terms] = {[round(v, 4) for v in t.tolist()]} s; "
+                   f"extrapolated to N={a.n} by N^2 / N^3 / N^2 / N^3 / N^2 -> {t_eval:.2f} s "
+                   f"per evaluation"),
+    }
+
+
+def _safe(f, *args):
+    try:
+        return f(*args)
+    except Exception as ex:  # never let the baseline leg kill the bench line
+        return {"value": None, "error": repr(ex)}
 
 
 def main():
@@ -141,6 +211,7 @@ def main():
             "potrf_TFLOPs": potrf_tf, "potri_TFLOPs_2n3_3": potri_tf,
             "grad_pass_GBps_Kinv_read": grad_gbs, "grad_pass_hbm_frac": grad_gbs / HBM_PEAK,
             "mll": mllv.value, "grad_finite": bool(np.isfinite(g).all()),
+            "cpu_baseline": None if (a.no_cpu_baseline or world > 1) else _safe(cpu_baseline, a, hp),
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -43,7 +43,74 @@ def parse():
                     help="variance for grid rows 1..var_rows (the reference's var_range; "
                          "SURVEY 8d: default 1:3 for parity, full 1:ne = 1024 for throughput)")
     ap.add_argument("--fit", default="broadcast", choices=["broadcast", "replicate"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-ns", type=int, default=4096,
+                    help="bounded CPU sample: the oracle's C5 job at this ns (same grid), each "
+                         "stage extrapolated to --ns by its complexity")
     return ap.parse_args()
+
+
+def cpu_baseline(a, hp, xe, xq):
+    """The CPU oracle (test infrastructure; this leg only) on a bounded sample of the C5 job:
+    predict(md, Cmap(+, xe, xq); diagonal_var=true) in the reference's order (src/predict.jl:
+    29-34 fit, src/split_predict.jl:5-53 split factors, mean, variance rows) at ns = a.cpu_ns on
+    the same 1024 x 1024 grid and variance rows, median of 3 after a warm-up; stages scaled to
+    ns = a.ns by their complexity (fit ns^3, split factors + mean ns, variance rows ns^2).
+    Threads: OMP_NUM_THREADS for OpenBLAS, reported by threadpoolctl."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+
+    sys.path.insert(0, ROOT)
+    from oracle import gpr_oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    ns, d = a.cpu_ns, a.d
+    kinds = [O.SE, O.WN]
+    x = np.random.default_rng(0).random((d, ns))
+    y = np.sin(x.sum(0)) ** 2
+    vr = (1, a.var_rows) if a.var_rows > 0 else None
+
+    def run():
+        t0 = time.perf_counter()
+        U = O.chol_upper(O.kernel(kinds, hp, x))
+        wt = O.cho_solve_upper(U, y)
+        t1 = time.perf_counter()
+        mu, _ = O.split_predict_from_factor(kinds, hp, x, U, wt, xe, xq, var_range=None)
+        t2 = time.perf_counter()
+        _, var = O.split_predict_from_factor(kinds, hp, x, U, wt, xe, xq, var_range=vr,
+                                             mean_rows=[0])
+        t3 = time.perf_counter()
+        assert np.isfinite(mu).all() and np.isfinite(var).all()
+        return np.array([t1 - t0, t2 - t1, t3 - t2])
+
+    with threadpool_limits(limits=threads):
+        blas = [{"lib": i.get("internal_api"), "version": i.get("version"),
+                 "threads": i.get("num_threads")}
+                for i in threadpool_info() if i.get("user_api") == "blas"
+                and "scipy.libs" in i.get("filepath", "")]
+        run()
+        reps = [run() for _ in range(3)]
+    t = np.median(np.stack(reps), axis=0)
+    r = a.ns / ns
+    scale = np.array([r ** 3, r, r ** 2])
+    t_job = float(np.sum(t * scale))
+    return {
+        "value": a.ne * a.nq / t_job, "unit": "test points/s", "cores": threads, "kind": "port",
+        "blas": blas,
+        "measured_config": {"ns": ns, "ne": a.ne, "nq": a.nq, "var_rows": a.var_rows,
+                            "stage_s": [round(v, 4) for v in t.tolist()]},
+        "sample": (f"oracle (NumPy/SciPy OpenBLAS, {threads} threads) C5 job at ns={ns}, "
+                   f"{a.ne}x{a.nq} grid, {a.var_rows} variance rows (median of 3 after 1 "
+                   f"warm-up): stages [fit, split factors + mean, variance rows] = "
+                   f"{[round(v, 4) for v in t.tolist()]} s; extrapolated to ns={a.ns} by ns^3 / "
+                   f"ns / ns^2 -> {t_job:.2f} s per job"),
+    }
+
+
+def _safe(f, *args):
+    try:
+        return f(*args)
+    except Exception as ex:  # never let the baseline leg kill the bench line
+        return {"value": None, "error": repr(ex)}
 
 
 def main():
@@ -141,6 +208,7 @@ def main():
                           if cls["dag_solve"][1] else None),
             "fit_dag_ms_per_step": cls["dag_fit"][0] / a.steps,
             "results_finite": bool(np.isfinite(mu).all() and np.isfinite(var).all()),
+            "cpu_baseline": None if (a.no_cpu_baseline or world > 1) else _safe(cpu_baseline, a, hp, xe, xq),
         })
         os.write(json_fd, (line + "\n").encode())
     dist.barrier()

@@ -26,15 +26,11 @@ constexpr int KT = 64;  // output tile edge
 
 // 16-B stores need a 16-B aligned K and an even leading dimension (GPR_KBUILD_SCALAR forces
 // the 8-B-store kernels, for A/B runs)
-// persistent grid of the 16-B-store kernels: workgroups per CU x 256 CUs (GPR_KBUILD_WGS)
-inline long long kbuild_grid() {
-  static const long long g = 256LL * (getenv("GPR_KBUILD_WGS") ? atoi(getenv("GPR_KBUILD_WGS")) : 8);
-  return g;
-}
+// persistent grid of the 16-B-store kernels: 8 workgroups per CU x 256 CUs
+inline long long kbuild_grid() { return 256LL * 8; }
 
 inline bool vec_store_ok(const double* K, int ldk) {
-  static const bool off = getenv("GPR_KBUILD_SCALAR") != nullptr;
-  return !off && ((uintptr_t)K & 15) == 0 && (ldk & 1) == 0;
+  return ((uintptr_t)K & 15) == 0 && (ldk & 1) == 0;
 }
 
 // xs[p][k + a*d] = x[k + a*d] * l_p[k]   (x .* ls[:, n], src/covariance.jl:90)
@@ -967,10 +963,9 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
   }
 }
 
-inline bool gram_enabled(int d) {
-  static const bool exact = getenv("GPR_KBUILD_EXACT") != nullptr;
-  return !exact && d <= 4 * 5;
-}
+// the Gram form (MFMA distance) for d <= 20 unless the context asks for the reference's
+// difference form (GPR_KBUILD_EXACT knob)
+inline bool gram_enabled(const gpr_ctx* ctx, int d) { return !ctx->kbuild_exact && d <= 4 * 5; }
 
 template <int S>
 int launch_gram(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, const double* xps,
@@ -1029,15 +1024,23 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
   double* A = ctx->dgA;
   double* nrmA = A + opA;
   double* B = nrmA + nA;
-  static const int wgs = getenv("GPR_KBUILD_UWGS") ? atoi(getenv("GPR_KBUILD_UWGS")) : 8;
-  static const bool xcd = getenv("GPR_KBUILD_XCD") ? atoi(getenv("GPR_KBUILD_XCD")) != 0 : true;
-  if (ctx->kup_items_n != 2 * n + full) {  // work list: strip-major (bj << 16 | segment)
+  constexpr int wgs = 8;  // workgroups per CU of the persistent grid
+  // work list, cached per (n, full) in a few slots (fold and prior builds of cross-validation
+  // alternate two shapes): rebuilding one costs a sync, a free and a blocking copy
+  const long long key = 2LL * n + full;
+  gpr_ctx::KupList* kl = nullptr;
+  for (auto& e : ctx->kup)
+    if (e.key == key) kl = &e;
+  if (!kl) {  // strip-major (bj << 16 | segment), into the least recently used slot
+    kl = &ctx->kup[0];
+    for (auto& e : ctx->kup)
+      if (e.used < kl->used) kl = &e;
     std::vector<int> items;
     for (int bj = 0; bj * KU_W < n; ++bj) {
       const int rows = full ? n : kup_rows(bj * KU_W, n);
       for (int sg = 0; sg * KU_SEG < rows; ++sg) items.push_back((bj << 16) | sg);
     }
-    if (xcd) {
+    {
       // XCD-aware order: wave w of workgroup b takes items t = 4 b + w (mod 4 grid), and
       // workgroups b, b + 8, ... share an XCD (its L2).  Give the workgroups of each residue
       // b mod 8 the segments sg = residue (mod 8), still strip-major: each XCD then reads one
@@ -1055,18 +1058,19 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
         items[t] = q[g][pos[g]++];
       }
     }
-    if (ctx->kup_items) {
+    if (kl->d) {  // (an earlier launch on the stream may still read the evicted list)
       HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-      HIP_TRY(ctx, hipFree(ctx->kup_items));
-      ctx->kup_items = nullptr;
+      HIP_TRY(ctx, hipFree(kl->d));
+      kl->d = nullptr;
     }
-    ctx->kup_items_n = -1;
-    HIP_TRY(ctx, hipMalloc((void**)&ctx->kup_items, items.size() * sizeof(int)));
-    HIP_TRY(ctx, hipMemcpy(ctx->kup_items, items.data(), items.size() * sizeof(int),
+    kl->key = -1;
+    HIP_TRY(ctx, hipMalloc((void**)&kl->d, items.size() * sizeof(int)));
+    HIP_TRY(ctx, hipMemcpy(kl->d, items.data(), items.size() * sizeof(int),
                            hipMemcpyHostToDevice));
-    ctx->kup_nitems = (int)items.size();
-    ctx->kup_items_n = 2 * n + full;
+    kl->nitems = (int)items.size();
+    kl->key = key;
   }
+  kl->used = ++ctx->kup_clock;
   gram_center_kernel<<<NSE * d, 256, 0, ctx->stream>>>(xs, n, d, ctx->dgc);
   {
     const size_t total = opA;
@@ -1075,9 +1079,9 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
     gram_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(xs, n, d, S, nbA, NSE, ctx->dgc, 1.0, B, nullptr);
   }
   LAUNCH_CHECK(ctx);
-  const int grid = std::max(1, std::min((ctx->kup_nitems + 3) / 4, 256 * wgs));
+  const int grid = std::max(1, std::min((kl->nitems + 3) / 4, 256 * wgs));
   kmat_symu_kernel<S, NSE><<<grid, 256, sizeof(double) * (256 + 4 * KU_W) * NSE, ctx->stream>>>(
-      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, ctx->kup_items, ctx->kup_nitems, full);
+      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, kl->d, kl->nitems, full);
   LAUNCH_CHECK(ctx);
   return 0;
 }
@@ -1170,17 +1174,17 @@ int launch_kernel_matrix(gpr_ctx* ctx, const KParams& kp, const double* dX, int 
     // one SE part: both halves computed by the column build (store-bound: one exponential per
     // element is cheaper than the mirrored tiles' store pattern); more parts: upper tiles
     // computed once and mirrored through LDS (the exponentials dominate)
-    if (gram_enabled(kp.d) && kp.nse <= std::min(ctx->kbuild_full_cols_nse, 2))
+    if (gram_enabled(ctx, kp.d) && kp.nse <= 1)
       return kp.nse == 1 ? launch_gram_upper_s<1>(ctx, kp, ctx->dxs, n, dK, ldk, 1)
                          : launch_gram_upper_s<2>(ctx, kp, ctx->dxs, n, dK, ldk, 1);
-    if (gram_enabled(kp.d) && vec_store_ok(dK, ldk))
+    if (gram_enabled(ctx, kp.d) && vec_store_ok(dK, ldk))
       return launch_gram_any(ctx, kp, ctx->dxs, n, nullptr, n, 1, dK, ldk);
     DISPATCH_D(launch_sym, ctx, kp, ctx->dxs, n, dK, ldk);
     LAUNCH_CHECK(ctx);
   } else {
     GPR_TRY(scale_inputs(ctx, kp, dXp, m, &ctx->dxps, &ctx->xps_cap));
     TimerScope ts(ctx, TC_OTHER, 0.0);
-    if (gram_enabled(kp.d) && vec_store_ok(dK, ldk))
+    if (gram_enabled(ctx, kp.d) && vec_store_ok(dK, ldk))
       return launch_gram_any(ctx, kp, ctx->dxs, n, ctx->dxps, m, 0, dK, ldk);
     DISPATCH_D(launch_cross, ctx, kp, ctx->dxs, n, ctx->dxps, m, dK, ldk);
     LAUNCH_CHECK(ctx);
@@ -1193,7 +1197,7 @@ int launch_kernel_matrix_for_factor(gpr_ctx* ctx, const KParams& kp, const doubl
   ctx->kup_ptr = nullptr;
   // upper-only where the tile-DAG will take exactly this matrix directly (potrf_core), with
   // the Gram form (d <= 20) and one or two SE parts; the full symmetric K otherwise
-  const bool upper = ctx->kbuild_upper && n > 0 && gram_enabled(kp.d) && kp.nse <= 2 &&
+  const bool upper = ctx->kbuild_upper && n > 0 && gram_enabled(ctx, kp.d) && kp.nse <= 2 &&
                      dag_takes_whole(ctx, n, ldk, dK) && dag_shape_ok(n, ldk, dK);
   if (!upper) return launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, dK, ldk);
   GPR_TRY(scale_inputs(ctx, kp, dX, n, &ctx->dxs, &ctx->xs_cap));

@@ -51,13 +51,6 @@ struct gpr_ctx {
   int nb2 = 1024;  // outer panel width = K of the big trailing updates (multiple of nb)
   hipStream_t ls = nullptr;       // stream the launch helpers enqueue on (default: stream)
   hipStream_t stream2 = nullptr;  // lookahead panel stream (GEMMs of the panel chain)
-  hipStream_t stream3 = nullptr;  // inner lookahead: panel-update remainder beside the chain
-  int panel_mode = 0;             // 2: square chain + left-looking strip, 3: + inverse strip
-                                  // for strips >= inv_strip_min columns (GPR_PANEL)
-  int inv_strip_min = 12288;      // GPR_INV_STRIP_MIN
-  int inner_la = 0;               // split the panel inner update (GPR_INNER_LA=1; no gain measured)
-  hipStream_t sdiag = nullptr;    // diag-block kernels: CU-masked to a few reserved CUs
-  hipStream_t smain = nullptr;    // big trailing updates: CU mask = all but the reserved CUs
   hipStream_t srhs = nullptr;     // right-hand-side solves fused into the factorisation
   hipStream_t ssq = nullptr;      // square inverses of finished outer panels (fused solves)
   // gpr_fit_predict: 0 = factor, then solve (default); 1 / 2 = solve inside the factorisation
@@ -65,7 +58,7 @@ struct gpr_ctx {
   int fused_rhs = -1;             // gpr_fit_predict: -1 auto (fused, mode 2, when the tile-DAG
                                   // factors or n <= fused_rhs_nmax), 0 off, 1/2 forced
                                   // (GPR_FUSED_RHS)
-  int fused_rhs_nmax = 16384;     // GPR_FUSED_RHS_NMAX
+  int fused_rhs_nmax = 16384;
   int fuse_y = 1;                 // gpr_fit: z = U^{-T} y inside the factorisation, then the
                                   // backward sweep alone (GPR_FUSE_Y=0: both sweeps after it;
                                   // C5's fit on one GPU: 727 -> 714 ms per job)
@@ -73,22 +66,14 @@ struct gpr_ctx {
                                   // inside the factorisation (1), and K^{-1} = Z^T Z too (2) --
                                   // tile-DAG right-hand-side and gram tasks, or the blocked
                                   // factorisation's lookahead bubbles
-  int diag_cus = 0;               // number of CUs reserved for sdiag (0: no masking)
-  int syrk_pieces = 1;            // launches per big trailing SYRK (lookahead dispatch)
-  // persistent tile-DAG factorisation (dag.hip): 0 off, 1 on for dag_nmin <= n <= dag_nmax
-  // (GPR_DAG, GPR_DAG_NMIN, GPR_DAG_NMAX); the task list is cached per (tiles, rhs tiles).
+  // persistent tile-DAG factorisation (dag.hip): 0 off (GPR_DAG=0: the blocked two-stream
+  // factorisation), 1 on; the task list is cached per (tiles, rhs tiles).
   // Measured (POTRF alone, blocked -> DAG): N = 8192 9.3 -> 6.8 ms, 16384 34.5 -> 25.0,
   // 32768 193 -> 173.4 (67.7 TF/s); C3 fit + predict in one DAG launch 321.8 -> 305.5 ms.
   int dag_mode = 1;
-  int dag_nmin = 0, dag_nmax = 1 << 30;
-  long long dag_spin_limit = 1ll << 25;  // DAG dependency wait bound in polls (~4 s); the
-                                        // GPR_DAG_SPIN_LIMIT environment variable overrides
-                                        // it per launch (tests force timeouts with it)
+  long long dag_spin_limit = 1ll << 25;  // DAG dependency wait bound in polls (~4 s); test
+                                        // builds let GPR_DAG_SPIN_LIMIT override it per launch
   int dag_zlag = 4;       // lower-triangular right-hand-side rows scheduled after A's row i + lag (GPR_DAG_ZLAG)
-  int dag_rlag = 0;       // other right-hand-side rows after A's row i + lag (GPR_DAG_RLAG;
-                          // 1, 2, 4 measured no faster for C2 / C3)
-  int dag_fearly = 0;     // diagonal tasks right behind the tile they wait for (GPR_DAG_FEARLY;
-                          // measured C2 -1..0 %, C4 -0.3 %, C3 +0.4 %: off)
   int dag_lag_built = -1;
   // one-shot hook of the next whole-matrix factorisation launch (kglob 0, not a solve), called
   // right after the kernel is enqueued with an event that completes once the launch's progress
@@ -147,9 +132,6 @@ struct gpr_ctx {
   size_t big_cap = 0;           // doubles
   double* dbig2 = nullptr;
   size_t big2_cap = 0;
-  int panel_sq = 0;             // square-panel factorisation (1 launch + 1 GEMM per panel;
-                                // GPR_PANEL_SQ=1; slower than per-block panels so far)
-  int* dsync = nullptr;         // inter-workgroup counters of the square-panel kernel
   double* dsqinv = nullptr;     // U_sq^{-1} of every outer panel square (nb2^2 per slot)
   size_t sqinv_cap = 0;         // doubles
   int sqinv_nb2 = 0;            // nb2 the slots were written with (0 = none valid)
@@ -177,8 +159,14 @@ struct gpr_ctx {
   // (strip << 16 | segment, built once per n) and the matrix it last left without its strict
   // lower off-diagonal tiles -- the next potrf_core on exactly that matrix has the tile-DAG
   // write them (DAG_MIRROR), or mirrors them first on any other path
-  int* kup_items = nullptr;
-  int kup_items_n = -1, kup_nitems = 0;
+  struct KupList {
+    long long key = -1;  // 2 n + full
+    int nitems = 0;
+    int* d = nullptr;
+    unsigned long long used = 0;
+  };
+  KupList kup[4];
+  unsigned long long kup_clock = 0;
   const double* kup_ptr = nullptr;
   int kup_n = 0, kup_ld = 0;
   double* dagb = nullptr;       // batched tile-DAG workspace (W slots, task lists, counters)
@@ -186,8 +174,12 @@ struct gpr_ctx {
   double* deig = nullptr;       // block-Jacobi eigensolver workspace (eigen.hip)
   size_t eig_cap = 0;
   int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)
-  int kbuild_full_cols_nse = 1; // full symmetric K by the column build (both halves computed)
-                                // for up to this many SE parts (GPR_KBUILD_FULLCOLS; 0: off)
+  int kbuild_exact = 0;         // GPR_KBUILD_EXACT=1: the reference's difference form for K
+  int cv_batch = 1;             // GPR_CV_BATCH=0: cv_batch folds one by one on child contexts
+  double cv_batch_gb = 16.0;    // GPR_CV_BATCH_GB: device-memory budget of a batched launch
+  double quad_batch_gb = 16.0;  // GPR_QUAD_BATCH_GB: the same for the quadrature's columns
+  int quad_eigen = -1;          // GPR_QUAD_EIGEN: sample_noise quadrature path (-1 auto)
+  int quad_seq = 0;             // GPR_QUAD_SEQ=1: its per-column factorisations one at a time
 
   bool timing = false;
   std::vector<TimedLaunch> pending;
@@ -205,6 +197,8 @@ int split_predict_pieces(gpr_ctx* ctx, const int* kinds, int nk, const double* h
                          int npieces, int var_lo, int var_hi, double eps, double* dmu, int ldmu,
                          double* dvar, bool compact);
 int set_err(gpr_ctx* ctx, int code, const char* fmt, ...);
+// the knob values of `from` onto `to` (child contexts follow their parent)
+void copy_knobs(const gpr_ctx* from, gpr_ctx* to);
 
 #define HIP_TRY(ctx, expr)                                                          \
   do {                                                                              \

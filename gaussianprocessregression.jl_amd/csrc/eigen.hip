@@ -505,28 +505,18 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
     HIP_TRY(ctx, hipMemcpy2DAsync(Bp, (size_t)n2 * sizeof(double), dB, (size_t)ldb * sizeof(double),
                                   (size_t)n * sizeof(double), m, hipMemcpyDeviceToDevice, s));
   }
-  static const int max_sweeps = getenv("GPR_EIG_MAX_SWEEPS") ? atoi(getenv("GPR_EIG_MAX_SWEEPS")) : 60;
-  static const int max_inner = getenv("GPR_EIG_INNER") ? atoi(getenv("GPR_EIG_INNER")) : 1;
-  static const int reorth = getenv("GPR_EIG_REORTH") ? atoi(getenv("GPR_EIG_REORTH")) : 1;
-  static const bool merged = getenv("GPR_EIG_SUBK") ? atoi(getenv("GPR_EIG_SUBK")) != 0 : true;
-  static const bool tmfma = getenv("GPR_EIG_TMFMA") ? atoi(getenv("GPR_EIG_TMFMA")) != 0 : true;
-  static const bool skipi = getenv("GPR_EIG_SKIPI") ? atoi(getenv("GPR_EIG_SKIPI")) != 0 : true;
+  // (measured variants -- the unmerged 256-thread subproblem, the VALU round transform, no
+  // identity skipping, more inner sweeps -- were all slower; round 4)
+  constexpr int max_sweeps = 60, max_inner = 1, reorth = 1;
   const int nch = m > 0 ? (m + ES - 1) / ES : 0;
   int sweep = 0, hrot = 1;
   TimerScope ts(ctx, TC_OTHER, 0.0);
   for (; sweep < max_sweeps && hrot; ++sweep) {
     HIP_TRY(ctx, hipMemsetAsync(rot, 0, sizeof(int), s));
     for (int r = 0; r < nb - 1; ++r) {
-      if (merged)
-        eig_subproblem_kernel<true, 1024><<<np, 1024, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth, floor);
-      else
-        eig_subproblem_kernel<false, 256><<<np, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth, 0.0);
-      if (tmfma)
-        eig_transform_kernel<true><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
-                                                                    (size_t)n2, m, ntiles, skipi ? rot + 2 : nullptr);
-      else
-        eig_transform_kernel<false><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
-                                                                     (size_t)n2, m, ntiles, skipi ? rot + 2 : nullptr);
+      eig_subproblem_kernel<true, 1024><<<np, 1024, 0, s>>>(W, (size_t)n2, nb, r, Rb, rot, max_inner, reorth, floor);
+      eig_transform_kernel<true><<<ntiles + np * nch, 256, 0, s>>>(W, (size_t)n2, nb, r, Rb, Bp,
+                                                                  (size_t)n2, m, ntiles, rot + 2);
     }
     LAUNCH_CHECK(ctx);
     HIP_TRY(ctx, hipMemcpyAsync(&hrot, rot, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -43,7 +43,6 @@ struct GemmK {
   int gm, gn;           // super-tile edges (tiles)
   int xcd_remap;
   int super_m;          // super-tiles along m (general grid)
-  int dbg;              // diagnostics: every tile loads the first panels (L2-resident)
 };
 
 __device__ __forceinline__ bool tile_coords(const GemmK& a, int& m0, int& n0) {
@@ -213,7 +212,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(GemmK a) {
         const int idx = tid + 256 * r;
         const int col = idx >> 3, k = k0 + 2 * (idx & 7);
         const int kc = k < kend ? k : kbeg;
-        const int m = min((a.dbg ? 0 : m0) + col, g.M - 1), n = min((a.dbg ? 0 : n0) + col, g.N - 1);
+        const int m = min(m0 + col, g.M - 1), n = min(n0 + col, g.N - 1);
         vp[r] = *reinterpret_cast<const d2*>(g.P + (size_t)kc + (size_t)m * g.ldp);
         vq[r] = *reinterpret_cast<const d2*>(g.Q + (size_t)kc + (size_t)n * g.ldq);
       }
@@ -482,7 +481,6 @@ __device__ __forceinline__ void gemm_tn_pipe_body(const GemmK& a) {
   gemm_epilogue(g, acc, m0, n0, lds + PBUF * STAGE_D, PRELOAD);
 }
 
-__global__ __launch_bounds__(256, 1) void gemm_tn_pipe16_kernel(GemmK a) { gemm_tn_pipe_body<16, false>(a); }
 // pipe8: C preloaded (beta != 0, the SYRK / TRSM updates); pipe8z: zero-initialised
 __global__ __launch_bounds__(256, 2) void gemm_tn_pipe8_kernel(GemmK a) { gemm_tn_pipe_body<8, true>(a); }
 __global__ __launch_bounds__(256, 2) void gemm_tn_pipe8z_kernel(GemmK a) { gemm_tn_pipe_body<8, false>(a); }
@@ -610,23 +608,6 @@ __global__ __launch_bounds__(256, 4) void gemm_tn_narrow_kernel(GemmK a) {
 
 }  // namespace
 
-// GPR_GEMM_PIPE: 1 = the 1-WG/CU variant, 2 (default) = the 2-WG/CU variant (faster at every
-// measured shape: 74.3 vs 71.9 TF/s at 8192^3, 66.3 vs 52.0 at 16384^2 x 768), 3 = by K
-static int pipe_env() {
-  static const int m = getenv("GPR_GEMM_PIPE") ? atoi(getenv("GPR_GEMM_PIPE")) : 2;
-  return m;
-}
-
-static bool pipe_off() {
-  static const bool off = getenv("GPR_GEMM_NOPIPE") != nullptr;
-  return off;
-}
-
-static bool vec_off() {
-  static const bool off = getenv("GPR_GEMM_SCALAR") != nullptr;
-  return off;
-}
-
 int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   if (g.M <= 0 || g.N <= 0) return 0;
   if (g.norm_out && g.M > TM) return set_err(ctx, GPR_E_ARG, "gemm norm epilogue needs M<=%d", TM);
@@ -634,14 +615,11 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   a.g = g;
   a.tiles_m = (g.M + TM - 1) / TM;
   a.tiles_n = (g.N + TN - 1) / TN;
-  static const int genv = getenv("GPR_GEMM_GROUP") ? atoi(getenv("GPR_GEMM_GROUP")) : 8;
-  static const int xenv = getenv("GPR_GEMM_XCD") ? atoi(getenv("GPR_GEMM_XCD")) : 1;
+  constexpr int genv = 8;  // super-tile edge (tiles) of the XCD-aware walk
   // the XCD remap hands each XCD a contiguous range of tiles (L2 locality); with per-tile
   // K ranges (kfrom_n / kend_from_m) that range would hold all the heavy tiles of one end
   // of the triangle, so those launches keep the round-robin dispatch order (balanced XCDs)
-  a.xcd_remap = xenv && !g.kfrom_n && !g.kend_from_m;
-  static const int dbg = getenv("GPR_GEMM_DBG_L2") ? 1 : 0;
-  a.dbg = dbg;
+  a.xcd_remap = !g.kfrom_n && !g.kend_from_m;
   a.gm = std::max(1, std::min(genv, a.tiles_m));
   a.gn = std::max(1, std::min(genv, a.tiles_n));
   if (g.upper) a.gn = a.gm;
@@ -668,16 +646,13 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
   TimerScope ts(ctx, timing_class, flops);
   // g.occ1: reserve LDS so only ONE such workgroup fits per CU, leaving the other half of
   // every CU to a concurrent (lookahead) stream
-  static const size_t pad_env = getenv("GPR_GEMM_PAD") ? (size_t)atoi(getenv("GPR_GEMM_PAD")) : 0;
-  const size_t pad = g.occ1 ? 20 * 1024 : pad_env;
+  const size_t pad = g.occ1 ? 20 * 1024 : 0;
   const bool vec = !g.qscale && ((uintptr_t)g.P & 15) == 0 && ((uintptr_t)g.Q & 15) == 0 &&
-                   (g.ldp & 1) == 0 && (g.ldq & 1) == 0 && (g.K & 1) == 0 &&
-                   !vec_off();
+                   (g.ldp & 1) == 0 && (g.ldq & 1) == 0 && (g.K & 1) == 0;
   // pipelined variants need K - kbeg to be a whole number of stages (kbeg is 0 or a
-  // multiple of TN); long K goes to the one-workgroup-per-CU variant
-  // few 128 x 128 tiles at short K: the narrow-tile kernel spreads them over 4x the CUs
-  // (GPR_GEMM_NARROW = max 128x128 tiles for it, default 384; 0 disables)
-  static const int narrow_max = getenv("GPR_GEMM_NARROW") ? atoi(getenv("GPR_GEMM_NARROW")) : 384;
+  // multiple of TN).  Few 128 x 128 tiles at short K: the narrow-tile kernel spreads them
+  // over 4x the CUs (up to 384 tiles)
+  constexpr int narrow_max = 384;
   if (vec && !g.occ1 && !g.E && !g.norm_out && g.K <= 256 && nblk <= narrow_max &&
       !(g.upper && g.kfrom_n)) {
     GemmK an = a;
@@ -687,15 +662,12 @@ int launch_gemm_tn(gpr_ctx* ctx, const GemmArgs& g, int timing_class) {
     LAUNCH_CHECK(ctx);
     return 0;
   }
-  const int pipe_mode = pipe_off() ? 0 : pipe_env();
-  const bool pipe = vec && (g.K % TK) == 0 && !g.occ1 && pipe_mode != 0;
-  const bool long_k = pipe_mode == 1 || (pipe_mode == 3 && g.K >= 2048);
-  if (pipe && long_k)
-    gemm_tn_pipe16_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
-  else if (pipe) {
-    static const bool nopre = getenv("GPR_GEMM_NOPRELOAD") != nullptr;
+  // the pipelined 2-WG/CU kernel (faster than its 1-WG/CU, 16-deep form at every measured
+  // shape: 74.3 vs 71.9 TF/s at 8192^3, 66.3 vs 52.0 at 16384^2 x 768)
+  const bool pipe = vec && (g.K % TK) == 0 && !g.occ1;
+  if (pipe) {
     TimerScope tk(ctx, TC_GEMM_PIPE, flops);
-    if (g.beta != 0.0 && g.alpha != 0.0 && !g.E && !nopre)
+    if (g.beta != 0.0 && g.alpha != 0.0 && !g.E)
       gemm_tn_pipe8_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);
     else
       gemm_tn_pipe8z_kernel<<<(unsigned)nblk, 256, 0, ctx->ls>>>(a);

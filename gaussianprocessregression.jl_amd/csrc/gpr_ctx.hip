@@ -122,6 +122,64 @@ int make_kparams(gpr_ctx* ctx, const int* kinds, int nk, const double* hp, int d
   return 0;
 }
 
+// ---- knobs ---------------------------------------------------------------------------------
+// Every run-time switch of the library: a GPR_* environment variable read once by
+// gpr_ctx_create, or gpr_set_knob on a live context.  Documented in include/gpr_hip.h; none of
+// them changes a result beyond rounding (they pick between equivalent code paths or tune
+// memory budgets).  Test-only fault injection exists only in libgpr_hip_testing.so
+// (-DGPR_TESTING).
+namespace {
+struct Knob {
+  const char* name;
+  int gpr_ctx::*ip;     // an int field, or
+  double gpr_ctx::*dp;  // a double field
+};
+const Knob kKnobs[] = {
+    {"GPR_DAG", &gpr_ctx::dag_mode, nullptr},
+    {"GPR_DAG_TAIL", &gpr_ctx::dag_tail, nullptr},
+    {"GPR_DAG_SOLVE", &gpr_ctx::dag_solve, nullptr},
+    {"GPR_DAG_GRAM", &gpr_ctx::dag_gram, nullptr},
+    {"GPR_DAG_ZLAG", &gpr_ctx::dag_zlag, nullptr},
+    {"GPR_FUSED_RHS", &gpr_ctx::fused_rhs, nullptr},
+    {"GPR_FUSE_Y", &gpr_ctx::fuse_y, nullptr},
+    {"GPR_FUSE_KINV", &gpr_ctx::fuse_kinv, nullptr},
+    {"GPR_KBUILD_UPPER", &gpr_ctx::kbuild_upper, nullptr},
+    {"GPR_KBUILD_EXACT", &gpr_ctx::kbuild_exact, nullptr},
+    {"GPR_CV_STREAMS", &gpr_ctx::cv_streams, nullptr},
+    {"GPR_CV_BATCH", &gpr_ctx::cv_batch, nullptr},
+    {"GPR_CV_BATCH_GB", nullptr, &gpr_ctx::cv_batch_gb},
+    {"GPR_QUAD_BATCH_GB", nullptr, &gpr_ctx::quad_batch_gb},
+    {"GPR_QUAD_EIGEN", &gpr_ctx::quad_eigen, nullptr},
+    {"GPR_QUAD_SEQ", &gpr_ctx::quad_seq, nullptr},
+};
+
+void knob_set(gpr_ctx* ctx, const Knob& k, double v) {
+  if (k.ip) {
+    int iv = (int)v;
+    if (k.ip == &gpr_ctx::dag_zlag) iv = std::max(0, iv);
+    if (k.ip == &gpr_ctx::cv_streams) iv = std::max(1, std::min(iv, (int)gpr_ctx::CV_MAX_SUB));
+    ctx->*k.ip = iv;
+  } else {
+    ctx->*k.dp = v;
+  }
+}
+
+const Knob* knob_find(const char* name) {
+  if (!name) return nullptr;
+  for (const Knob& k : kKnobs)
+    if (!strcmp(k.name, name)) return &k;
+  return nullptr;
+}
+}  // namespace
+
+void copy_knobs(const gpr_ctx* from, gpr_ctx* to) {
+  for (const Knob& k : kKnobs) {
+    if (k.ip) to->*k.ip = from->*k.ip;
+    else to->*k.dp = from->*k.dp;
+  }
+  to->dag_spin_limit = from->dag_spin_limit;
+}
+
 extern "C" {
 
 const char* gpr_version(void) { return "gpr_hip 0.1.0 (gfx950)"; }
@@ -150,20 +208,11 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
   int prio_lo = 0, prio_hi = 0;
   hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->srhs, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->ssq, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return GPR_E_HIP;
   }
-  if (const char* e = getenv("GPR_FUSED_RHS")) ctx->fused_rhs = atoi(e);
-  if (const char* e = getenv("GPR_FUSED_RHS_NMAX")) ctx->fused_rhs_nmax = atoi(e);
-  if (const char* e = getenv("GPR_FUSE_Y")) ctx->fuse_y = atoi(e);
-  if (const char* e = getenv("GPR_FUSE_KINV")) ctx->fuse_kinv = atoi(e);
-  if (const char* e = getenv("GPR_NB2")) ctx->nb2 = atoi(e);
-  if (const char* e = getenv("GPR_SYRK_PIECES")) ctx->syrk_pieces = atoi(e);
-  if (const char* e = getenv("GPR_PANEL_SQ")) ctx->panel_sq = atoi(e);
-  if (const char* e = getenv("GPR_INNER_LA")) ctx->inner_la = atoi(e);
   // Concurrent child contexts of cv_batch / integrate_noise: each drives its own stream, so
   // by default no more of them than the process has hardware queues (GPU_MAX_HW_QUEUES,
   // HIP's default 4); more only multiplex onto the same queues.
@@ -171,48 +220,9 @@ int gpr_ctx_create(int device, void* stream, gpr_ctx_t* out) {
     const int q = atoi(e);
     if (q > 0) ctx->cv_streams = std::min(ctx->cv_streams, q);
   }
-  if (const char* e = getenv("GPR_PANEL")) ctx->panel_mode = atoi(e);
-  if (const char* e = getenv("GPR_DAG")) ctx->dag_mode = atoi(e);
-  if (const char* e = getenv("GPR_KBUILD_UPPER")) ctx->kbuild_upper = atoi(e);
-  if (const char* e = getenv("GPR_KBUILD_FULLCOLS")) ctx->kbuild_full_cols_nse = atoi(e);
-  if (const char* e = getenv("GPR_DAG_NMIN")) ctx->dag_nmin = atoi(e);
-  if (const char* e = getenv("GPR_DAG_NMAX")) ctx->dag_nmax = atoi(e);
-  if (const char* e = getenv("GPR_DAG_TAIL")) ctx->dag_tail = atoi(e);
-  if (const char* e = getenv("GPR_DAG_SOLVE")) ctx->dag_solve = atoi(e);
-  if (const char* e = getenv("GPR_DAG_GRAM")) ctx->dag_gram = atoi(e);
-  if (const char* e = getenv("GPR_DAG_ZLAG")) ctx->dag_zlag = std::max(0, atoi(e));
-  if (const char* e = getenv("GPR_DAG_RLAG")) ctx->dag_rlag = std::max(0, atoi(e));
-  if (const char* e = getenv("GPR_DAG_FEARLY")) ctx->dag_fearly = atoi(e) != 0;
-  if (const char* e = getenv("GPR_INV_STRIP_MIN")) ctx->inv_strip_min = atoi(e);
-  if (const char* e = getenv("GPR_CV_STREAMS")) ctx->cv_streams = atoi(e);
-  // Reserve a few CUs for the latency-bound diag-block kernel of the factorisation: beside
-  // an MFMA-saturating trailing-update workgroup it runs ~6x slower (measured), and it is
-  // on the critical path of the lookahead chain.  GEMM streams get the complement mask.
-  ctx->diag_cus = 0;
-  if (const char* e = getenv("GPR_DIAG_CUS")) ctx->diag_cus = atoi(e);
-  if (ctx->diag_cus > 0) {
-    hipDeviceProp_t prop;
-    hipGetDeviceProperties(&prop, device);
-    const int ncu = prop.multiProcessorCount;
-    uint32_t md[16] = {0}, mr[16] = {0};
-    for (int c = 0; c < ncu && c < 512; ++c) {
-      if (c < ctx->diag_cus) md[c >> 5] |= 1u << (c & 31);
-      else mr[c >> 5] |= 1u << (c & 31);
-    }
-    const uint32_t words = (uint32_t)((ncu + 31) / 32);
-    if (hipExtStreamCreateWithCUMask(&ctx->sdiag, words, md) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&ctx->smain, words, mr) != hipSuccess) {
-      ctx->diag_cus = 0;
-    }
-    const char* pm = getenv("GPR_PANEL_MASK");
-    if (ctx->diag_cus > 0 && (!pm || atoi(pm))) {
-      hipStream_t s2m = nullptr;
-      if (hipExtStreamCreateWithCUMask(&s2m, words, mr) == hipSuccess) {
-        hipStreamDestroy(ctx->stream2);
-        ctx->stream2 = s2m;
-      }
-    }
-  }
+  // the documented knobs (include/gpr_hip.h), read once here; gpr_set_knob changes them
+  for (const Knob& k : kKnobs)
+    if (const char* e = getenv(k.name)) knob_set(ctx, k, atof(e));
   if (hipMalloc((void**)&ctx->dinfo, 64) != hipSuccess) {
     delete ctx;
     return GPR_E_NOMEM;
@@ -244,13 +254,10 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto e : ctx->sync_events) hipEventDestroy(e);
   if (ctx->stream2) hipStreamDestroy(ctx->stream2);
-  if (ctx->stream3) hipStreamDestroy(ctx->stream3);
   if (ctx->srhs) hipStreamDestroy(ctx->srhs);
   if (ctx->ssq) hipStreamDestroy(ctx->ssq);
   if (ctx->dpanel_rhs) hipFree(ctx->dpanel_rhs);
   if (ctx->dscr_wt) hipFree(ctx->dscr_wt);
-  if (ctx->sdiag) hipStreamDestroy(ctx->sdiag);
-  if (ctx->smain) hipStreamDestroy(ctx->smain);
   if (ctx->dag_tasks) hipFree(ctx->dag_tasks);
   if (ctx->dag_sync) hipFree(ctx->dag_sync);
   if (ctx->dpadA) hipFree(ctx->dpadA);
@@ -263,7 +270,6 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dbig) hipFree(ctx->dbig);
   if (ctx->dbig2) hipFree(ctx->dbig2);
   if (ctx->dtrsv) hipFree(ctx->dtrsv);
-  if (ctx->dsync) hipFree(ctx->dsync);
   if (ctx->dsqinv) hipFree(ctx->dsqinv);
   if (ctx->dpanel) hipFree(ctx->dpanel);
   if (ctx->dxs) hipFree(ctx->dxs);
@@ -271,7 +277,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   if (ctx->dgA) hipFree(ctx->dgA);
   if (ctx->dgB) hipFree(ctx->dgB);
   if (ctx->dgc) hipFree(ctx->dgc);
-  if (ctx->kup_items) hipFree(ctx->kup_items);
+  for (auto& e : ctx->kup)
+    if (e.d) hipFree(e.d);
   if (ctx->deig) hipFree(ctx->deig);
   if (ctx->dagb) hipFree(ctx->dagb);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
@@ -325,6 +332,23 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2) {
   if (nb2 < ctx->nb || nb2 % ctx->nb)
     return set_err(ctx, GPR_E_ARG, "outer block %d must be a multiple of nb=%d", nb2, ctx->nb);
   ctx->nb2 = nb2;
+  return 0;
+}
+
+int gpr_set_knob(gpr_ctx_t ctx, const char* name, double value) {
+  if (!ctx) return GPR_E_ARG;
+  const Knob* k = knob_find(name);
+  if (!k) return set_err(ctx, GPR_E_ARG, "unknown knob %s", name ? name : "(null)");
+  knob_set(ctx, *k, value);
+  if (k->ip == &gpr_ctx::dag_zlag) ctx->dag_lag_built = -1;  // (the task list depends on it)
+  return 0;
+}
+
+int gpr_get_knob(gpr_ctx_t ctx, const char* name, double* value) {
+  if (!ctx || !value) return GPR_E_ARG;
+  const Knob* k = knob_find(name);
+  if (!k) return set_err(ctx, GPR_E_ARG, "unknown knob %s", name ? name : "(null)");
+  *value = k->ip ? (double)(ctx->*k->ip) : ctx->*k->dp;
   return 0;
 }
 

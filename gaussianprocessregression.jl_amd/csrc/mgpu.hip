@@ -219,6 +219,11 @@ struct gpr_mgpu {
   // (GPU_MAX_HW_QUEUES = 4) runs its work behind the launch, so everything goes on this one
   hipStream_t sp = nullptr;
   int* derr = nullptr;  // device 0: a gate timed out
+  // knobs, read from the environment once at gpr_mgpu_create (include/gpr_hip.h)
+  int stream_out = -1;   // GPR_MGPU_STREAM: U streamed out during device 0's fit (-1: only at ngpu 1)
+  int reserve_cu = 8;    // GPR_MGPU_RESERVE_CU: CUs the streamed fit's launch leaves free
+  int chunks = 16;       // GPR_MGPU_CHUNKS: tile-row chunks of the broadcast
+  int self_bcast = 0;    // GPR_MGPU_SELF_BCAST: ngpu 1 runs the broadcast protocol to itself
 };
 
 namespace {
@@ -409,6 +414,10 @@ int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out) {
   h->dev.assign(devices, devices + ngpu);
   h->ctx.assign(ngpu, nullptr);
   h->buf.resize(ngpu);
+  if (const char* e = getenv("GPR_MGPU_STREAM")) h->stream_out = atoi(e) != 0;
+  if (const char* e = getenv("GPR_MGPU_RESERVE_CU")) h->reserve_cu = atoi(e);
+  if (const char* e = getenv("GPR_MGPU_CHUNKS")) h->chunks = atoi(e);
+  if (const char* e = getenv("GPR_MGPU_SELF_BCAST")) h->self_bcast = atoi(e) != 0;
   for (int i = 0; i < ngpu; ++i) {
     for (int j = 0; j < i; ++j)
       if (h->dev[j] == h->dev[i]) {
@@ -425,17 +434,12 @@ int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out) {
     return GPR_E_HIP;
   }
   {
-    // low priority (GPR_MGPU_SP=normal / high: the others).  Measured (profiles/
-    // r03_mgpu_stream_out_trace.txt): low, normal and high priority streams all ran the
-    // stream-out inside the launch's window; a CU-masked stream ran it after the launch.
-    const char* e = getenv("GPR_MGPU_SP");
-    const std::string kind = e ? e : "low";
+    // low priority.  Measured (profiles/r03_mgpu_stream_out_trace.txt): low, normal and high
+    // priority streams all ran the stream-out inside the launch's window; a CU-masked stream
+    // ran it after the launch.
     int lo = 0, hi = 0;
     hipDeviceGetStreamPriorityRange(&lo, &hi);
-    const hipError_t r =
-        kind == "normal" ? hipStreamCreateWithFlags(&h->sp, hipStreamNonBlocking)
-                         : hipStreamCreateWithPriority(&h->sp, hipStreamNonBlocking,
-                                                       kind == "high" ? hi : lo);
+    const hipError_t r = hipStreamCreateWithPriority(&h->sp, hipStreamNonBlocking, lo);
     if (r != hipSuccess) {
       h->sp = nullptr;
       gpr_mgpu_destroy(h);
@@ -491,8 +495,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   const int G = h->ngpu;
   // GPR_MGPU_SELF_BCAST=1 (tests on a one-GPU box): the broadcast path even for one device,
   // which then also acts as a receiver (pack, 1-rank RCCL broadcast, unpack, forget)
-  const char* sb = getenv("GPR_MGPU_SELF_BCAST");
-  const bool self_bcast = sb && atoi(sb) != 0;
+  const bool self_bcast = h->self_bcast != 0;
   const bool bcast = fit_mode == GPR_MGPU_BROADCAST && (G > 1 || self_bcast);
   const size_t npk = packed_len(ns);
   std::vector<int> finfo(G, 0);
@@ -512,20 +515,20 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
   // chunk and wt trail the factorisation.  GPR_MGPU_STREAM default: streamed on one device (the
   // self-broadcast path the tests run), after the fit across devices -- no run with two or more
   // GPUs has exercised the streamed receivers yet; GPR_MGPU_STREAM=1 opts in there.
-  const char* e_st = getenv("GPR_MGPU_STREAM");
-  const bool stream = e_st ? atoi(e_st) != 0 : G == 1;
-  const char* e_rs = getenv("GPR_MGPU_RESERVE_CU");
-  const int reserve = e_rs ? std::max(0, atoi(e_rs)) : 8;
-  const char* e_ch = getenv("GPR_MGPU_CHUNKS");
-  const int maxc = e_ch ? std::max(1, atoi(e_ch)) : 16;
+  const bool stream = h->stream_out >= 0 ? h->stream_out != 0 : G == 1;
+  const int reserve = std::max(0, h->reserve_cu);
+  const int maxc = std::max(1, h->chunks);
   StreamOut so;
   so.h = h;
   so.n = ns;
   so.rows = row_chunks(ns, maxc);
   // (tests: GPR_MGPU_GATE_LIMIT=0 makes every gate give up at once -- the error path whatever
   // the factorisation's progress)
+#ifdef GPR_TESTING
+  // fault injection, test builds only (libgpr_hip_testing.so; tests/fault_scenarios.py)
   if (const char* e = getenv("GPR_MGPU_GATE_LIMIT")) so.limit = std::max(0ll, atoll(e));
   if (const char* e = getenv("GPR_MGPU_FAIL_UNPACK")) so.fail_unpack = atoi(e);
+#endif
   // 0. buffers and inputs on every device (a failure here stops every device before the
   //    broadcast protocol starts)
   auto rc = on_devices(h, [&](int i) -> int {

@@ -70,7 +70,7 @@ __device__ __forceinline__ void diag_block_body(double* __restrict__ A, size_t l
   __shared__ double rb[2][NB];
   __shared__ double wbuf[NW][SB];
   __shared__ int fail;
-  if (*info != 0 || mode == 3) return;  // mode 3: timing experiment only (GPR_DIAG_FAKE)
+  if (*info != 0) return;
   // this latency-bound chain shares CUs with the MFMA-saturating trailing update: take
   // issue priority over the co-resident GEMM waves (FP64 VALU and FP64 MFMA share the
   // SIMD's FP64 throughput on gfx950)
@@ -542,107 +542,6 @@ __device__ __forceinline__ void sq_store(const d4v (&acc)[4][4], double* C, size
         }
       }
 }
-
-// publish prog[c] = v after this workgroup's stores (guide: vmcnt drain, barrier, agent
-// release, relaxed flag store)
-__device__ __forceinline__ void sq_publish(int* prog, int c, int v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&prog[c], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// wait until prog[c] >= v (one lane polls; agent acquire; barrier).  Bounded: after ~4 s
-// of polling the factorisation is flagged (info = -1) and the wait gives up, so the grid
-// always drains.
-__device__ __forceinline__ void sq_wait(int* prog, int c, int v, int* info) {
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    long long spins = 0;
-    while (__hip_atomic_load(&prog[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++spins > (1ll << 24)) {
-        ok = 0;
-        break;
-      }
-    }
-    if (!ok) atomicCAS(info, 0, -1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(256, 1) void square_panel_kernel(double* __restrict__ A, size_t lda,
-                                                              int n, int k, int kw,
-                                                              double* __restrict__ winv,
-                                                              double* __restrict__ sqinv,
-                                                              int* __restrict__ info,
-                                                              int* __restrict__ sync) {
-  constexpr int NB = 128;
-  __shared__ int s_tile;
-  __shared__ double glds[2 * 4096];  // tile-product staging (64 KB)
-  // latency-bound chain beside the MFMA-saturating trailing update: take issue priority
-  __builtin_amdgcn_s_setprio(3);
-  if (threadIdx.x == 0) s_tile = atomicAdd(&sync[0], 1);
-  __syncthreads();
-  const int c = s_tile;
-  int* prog = sync + 1;
-  auto blk = [&](int i, int j) { return A + (size_t)(k + i * NB) + (size_t)(k + j * NB) * lda; };
-  auto wid = [&](int i) { return min(NB, kw - i * NB); };
-  auto W = [&](int i) { return winv + (size_t)((k / NB) + i) * NB * NB; };
-  const int cw = wid(c);
-  d4v acc[4][4];
-  for (int j = 0; j < c; ++j) {
-    const int jw = wid(j);
-    sq_wait(prog, j, j + 1, info);                       // U_jj, W_j final
-    sq_zero(acc);                                        // U(j, c) = W_j^T A(j, c)
-    sq_gemm<false>(acc, W(j), NB, blk(j, c), lda, jw, jw, cw, glds);
-    __syncthreads();                                     // in place: all reads first
-    sq_store(acc, blk(j, c), 1, lda, 1.0, 0.0, jw, cw, false);
-    sq_publish(prog, c, j + 1);
-    for (int i = j + 1; i <= c; ++i) {                   // A(i, c) -= U(j, i)^T U(j, c)
-      if (i < c) sq_wait(prog, i, j + 1, info);
-      sq_zero(acc);
-      sq_gemm<false>(acc, blk(j, i), lda, blk(j, c), lda, jw, wid(i), cw, glds);
-      sq_store(acc, blk(i, c), 1, lda, -1.0, 1.0, wid(i), cw, i == c);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  // step c: factor the diagonal block (own tile, updated by this workgroup only)
-  diag_block_body<NB>(A, lda, n, k + c * NB, info, W(c), 1, 0);
-  sq_publish(prog, c, c + 1);
-  // inverse, block column c
-  double* X = sqinv + (size_t)(c * NB) * kw;             // column block c of U_sq^{-1}
-  for (int e = threadIdx.x; e < NB * NB; e += 256) {
-    const int r = e % NB, q = e / NB;
-    if (r < cw && q < cw) X[(size_t)(c * NB + r) + (size_t)q * kw] = W(c)[r + (size_t)q * NB];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int i = c - 1; i >= 0; --i) {
-    const int iw = wid(i);
-    sq_zero(acc);                                        // S = sum_t U(i, t) X_tc
-    for (int t = i + 1; t <= c; ++t) {
-      if (t < c) sq_wait(prog, t, i + 1, info);
-      sq_gemm<true>(acc, blk(i, t), lda, X + t * NB, kw, wid(t), iw, cw, glds);
-    }
-    sq_store(acc, X + i * NB, 1, kw, 1.0, 0.0, iw, cw, false);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    sq_zero(acc);                                        // X_ic = -W_i S
-    sq_gemm<true>(acc, W(i), NB, X + i * NB, kw, iw, iw, cw, glds);
-    __syncthreads();
-    sq_store(acc, X + i * NB, 1, kw, -1.0, 0.0, iw, cw, false);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-}
-
 // ---- small-RHS triangular solves (TRSV-like, nrhs <= 16 per launch) --------------------
 constexpr int RHS_CHUNK = 16;
 
@@ -985,10 +884,7 @@ int launch_diag(gpr_ctx* ctx, double* A, int lda, int n, int kglob, double* winv
                 int nblocks) {
   const int nb = ctx->nb;
   TimerScope ts(ctx, TC_PANEL, 0.0);
-  static const bool fake = getenv("GPR_DIAG_FAKE") != nullptr;  // timing experiment only
-  static const bool v1 = getenv("GPR_DIAG_V1") != nullptr;
-  if (fake && mode == 1) mode = 3;
-  if (nb == 128 && mode == 1 && !v1 && nblocks == 1)
+  if (nb == 128 && mode == 1 && nblocks == 1)
     diag2_kernel<<<1, DIAG_THREADS, DIAG2_LDS, ctx->ls>>>(A, (size_t)lda, n, kglob, ctx->dinfo,
                                                        winv);
   else if (nb == 128)
@@ -1042,47 +938,15 @@ hipEvent_t sync_event(gpr_ctx* ctx, size_t i) {
 // Factor the rows [k, k+kw) of the (already updated) trailing matrix: per inner block j:
 // diag factor+inverse, in-place panel TRSM over all columns >= j+jb (MFMA GEMM with
 // U_jj^{-1}), then the update of the remaining rows of this outer panel (K = nb).
-static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
-
-static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
-
-static int factor_panel_inv(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
-static int factor_panel_rec(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw);
-
+// (Measured and removed in round 5: a square-chain + left-looking strip, an inverse strip,
+// recursive halves, inner / block lookahead, a one-launch square-panel kernel and CU masking
+// for the diagonal kernel -- every one slower than this per-block panel)
 int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
-  if (ctx->panel_mode == 3 && ctx->nb == 128 && ctx->diag_cus == 0 && !ctx->inner_la &&
-      n - k - kw >= std::max(1, ctx->inv_strip_min) && ctx->nb2 <= 2048 && ctx->nb2 >= 128)
-    return factor_panel_inv(ctx, A, n, lda, k, kw);
-  if (ctx->panel_mode == 4 && ctx->diag_cus == 0 && !ctx->inner_la)
-    return factor_panel_rec(ctx, A, n, lda, k, kw);
-  if (ctx->panel_mode == 2 && ctx->stream3 && ctx->diag_cus == 0 && !ctx->inner_la)
-    return factor_panel_ll(ctx, A, n, lda, k, kw);
-  if (ctx->inner_la == 2 && ctx->stream3 && ctx->diag_cus == 0)
-    return factor_panel_bla(ctx, A, n, lda, k, kw);
-  // Inner lookahead: after block j's row TRSM, only the NEXT strip (rows of block j+1) is
-  // updated on the chain stream; the remaining strips of the panel are updated on stream3
-  // beside diag(j+1) and TRSM(j+1).  Strip j+2 must hold that remainder update before the
-  // chain updates it at step j+1, so the chain waits for it there.
   const int nb = ctx->nb;
-  const bool la = ctx->inner_la && ctx->stream3;
-  hipStream_t home = ctx->ls, side = ctx->stream3;
-  hipEvent_t e_rest = nullptr;  // remainder update of the previous step (on side)
   for (int j = k; j < k + kw; j += nb) {
     const int jb = std::min(nb, n - j);
     double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
-    if (ctx->diag_cus > 0) {  // hop to the reserved-CU stream and back
-      hipEvent_t e1 = sync_event(ctx, ctx->ev_next++), e2 = sync_event(ctx, ctx->ev_next++);
-      HIP_TRY(ctx, hipEventRecord(e1, home));
-      HIP_TRY(ctx, hipStreamWaitEvent(ctx->sdiag, e1, 0));
-      ctx->ls = ctx->sdiag;
-      const int rc = launch_diag(ctx, A, lda, n, j, wj, 1, 1);
-      ctx->ls = home;
-      if (rc) return rc;
-      HIP_TRY(ctx, hipEventRecord(e2, ctx->sdiag));
-      HIP_TRY(ctx, hipStreamWaitEvent(home, e2, 0));
-    } else {
-      GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
-    }
+    GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
     if (j + jb >= n) break;
     double* row = A + j + (size_t)(j + jb) * lda;
     GemmArgs g{};
@@ -1095,331 +959,17 @@ int factor_panel(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
     GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
     const int rows = k + kw - j - jb;  // panel rows below block j
     if (rows <= 0) continue;
-    const int r1 = la ? std::min(nb, rows) : rows;
-    if (la && rows > r1) {
-      // remainder strips [j+jb+r1, k+kw) on the side stream, after this TRSM
-      hipEvent_t ex = sync_event(ctx, ctx->ev_next++);
-      HIP_TRY(ctx, hipEventRecord(ex, home));
-      HIP_TRY(ctx, hipStreamWaitEvent(side, ex, 0));
-      if (e_rest) HIP_TRY(ctx, hipStreamWaitEvent(side, e_rest, 0));
-      GemmArgs u2{};
-      u2.P = A + j + (size_t)(j + jb + r1) * lda; u2.ldp = lda;  // X_j columns of those rows
-      u2.Q = row; u2.ldq = lda;
-      u2.C = A + (j + jb + r1) + (size_t)(j + jb) * lda; u2.ldc = lda;
-      u2.M = rows - r1; u2.N = n - j - jb; u2.K = jb;
-      u2.alpha = -1.0; u2.beta = 1.0;
-      u2.mask_upper = 1; u2.mask_off = -r1;  // global row <= global column
-      u2.info = ctx->dinfo;
-      ctx->ls = side;
-      const int rc = launch_gemm_tn(ctx, u2, TC_PANEL);
-      ctx->ls = home;
-      if (rc) return rc;
-    }
-    // the next strip on the chain; it must already hold the previous remainder update
-    if (e_rest) {
-      HIP_TRY(ctx, hipStreamWaitEvent(home, e_rest, 0));
-      e_rest = nullptr;
-    }
     GemmArgs u{};
     u.P = row; u.ldp = lda;
     u.Q = row; u.ldq = lda;
     u.C = A + (j + jb) + (size_t)(j + jb) * lda; u.ldc = lda;
-    u.M = r1; u.N = n - j - jb; u.K = jb;
+    u.M = rows; u.N = n - j - jb; u.K = jb;
     u.alpha = -1.0; u.beta = 1.0;
     u.mask_upper = 1;
     u.info = ctx->dinfo;
     GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
-    if (la && rows > r1) {
-      e_rest = sync_event(ctx, ctx->ev_next++);
-      HIP_TRY(ctx, hipEventRecord(e_rest, side));
-    }
   }
-  if (e_rest) HIP_TRY(ctx, hipStreamWaitEvent(home, e_rest, 0));  // panel complete on home
   return 0;
-}
-
-// Square chain + left-looking strip (GPR_PANEL=2).  The inner blocks of the outer panel's
-// kw x kw diagonal square are factored on the chain stream with updates restricted to the
-// square (diag(j); U(j, square) = W_j^T A(j, square); A(square rows > j) -= U(j)^T U(j)):
-// the chain's GEMMs have at most 7 x 7 tiles, so they neither wait long for CU slots nor
-// take many from the trailing SYRK.  The strip right of the square (rows [k, k+kw), columns
-// [k+kw, n)) is solved block row by block row on the side stream, left-looking:
-//   B_i -= U(k:k+128i, i)^T R_{0:i}   (M = 128, N = n-k-kw, K = 128 i, beta = 1)
-//   R_i  = W_i^T B_i                  (in place, K = 128)
-// Step i needs only W_i and the square's column block i, both final once diag(i) ran, so the
-// strip trails the chain by one step instead of widening every chain GEMM to n - j columns
-// (whose K = 128 read-modify-write of up to 896 x n elements per step was the bulk of the
-// lookahead stream's time).  Same arithmetic as the right-looking panel up to summation order.
-static int factor_panel_ll(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
-  const int nb = ctx->nb;
-  hipStream_t home = ctx->ls, side = ctx->stream3;
-  const int kend = k + kw, nrest = n - kend;
-  int rc = 0;
-  auto gemm_on = [&](hipStream_t st, GemmArgs& g) {
-    ctx->ls = st;
-    const int r = launch_gemm_tn(ctx, g, TC_PANEL);
-    ctx->ls = home;
-    return r;
-  };
-  bool side_used = false;
-  for (int j = k; j < kend && !rc; j += nb) {
-    const int jb = std::min(nb, n - j);
-    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
-    if ((rc = launch_diag(ctx, A, lda, n, j, wj, 1, 1))) break;
-    if (nrest > 0) {  // strip step for block j on the side stream, after diag(j)
-      hipEvent_t ed = sync_event(ctx, ctx->ev_next++);
-      HIP_TRY(ctx, hipEventRecord(ed, home));
-      HIP_TRY(ctx, hipStreamWaitEvent(side, ed, 0));
-      side_used = true;
-      if (j > k) {
-        GemmArgs u{};
-        u.P = A + k + (size_t)j * lda; u.ldp = lda;          // U(k:j, block j)
-        u.Q = A + k + (size_t)kend * lda; u.ldq = lda;       // R_{0:i}
-        u.C = A + j + (size_t)kend * lda; u.ldc = lda;       // B_i
-        u.M = jb; u.N = nrest; u.K = j - k;
-        u.alpha = -1.0; u.beta = 1.0;
-        u.info = ctx->dinfo;
-        if ((rc = gemm_on(side, u))) break;
-      }
-      GemmArgs t{};
-      t.P = wj; t.ldp = nb;
-      t.Q = A + j + (size_t)kend * lda; t.ldq = lda;
-      t.C = A + j + (size_t)kend * lda; t.ldc = lda;
-      t.M = jb; t.N = nrest; t.K = jb;
-      t.alpha = 1.0; t.beta = 0.0;
-      t.info = ctx->dinfo;
-      if ((rc = gemm_on(side, t))) break;
-    }
-    const int c1 = j + jb;
-    if (c1 >= kend) break;
-    // chain: row j inside the square, then the square's rows below j
-    double* row = A + j + (size_t)c1 * lda;
-    GemmArgs g{};
-    g.P = wj; g.ldp = nb;
-    g.Q = row; g.ldq = lda;
-    g.C = row; g.ldc = lda;
-    g.M = jb; g.N = kend - c1; g.K = jb;
-    g.alpha = 1.0; g.beta = 0.0;
-    g.info = ctx->dinfo;
-    if ((rc = launch_gemm_tn(ctx, g, TC_PANEL))) break;
-    GemmArgs u{};
-    u.P = row; u.ldp = lda;
-    u.Q = row; u.ldq = lda;
-    u.C = A + c1 + (size_t)c1 * lda; u.ldc = lda;
-    u.M = kend - c1; u.N = kend - c1; u.K = jb;
-    u.alpha = -1.0; u.beta = 1.0;
-    u.upper = 1;
-    u.info = ctx->dinfo;
-    if ((rc = launch_gemm_tn(ctx, u, TC_PANEL))) break;
-  }
-  ctx->ls = home;
-  if (side_used) {  // panel complete on home
-    hipEvent_t es = sync_event(ctx, ctx->ev_next++);
-    HIP_TRY(ctx, hipEventRecord(es, side));
-    HIP_TRY(ctx, hipStreamWaitEvent(home, es, 0));
-  }
-  return rc;
-}
-
-// Square chain + inverse strip (GPR_PANEL=3, outer panels whose strip is at least
-// ctx->inv_strip_min columns wide).  The kw x kw diagonal square is factored on the chain
-// with updates restricted to the square (as factor_panel_ll); then U_sq^{-1} is formed from
-// the square and its block inverses (sqinv_kernel, one workgroup per block column) and the
-// strip right of the square is ONE K = kw GEMM, X = U_sq^{-T} A(k:k+kw, k+kw:n), with the
-// K range cut at each tile's diagonal (out of place, strided copy back).  The per-block
-// form spends the strip's kw^2 (n - k - kw) flops in K = 128 GEMMs that read-modify-write up
-// to 896 x (n - j) elements per step; beside the trailing SYRK those take CU time out of
-// proportion to their flops.  The inverse costs a latency of ~0.5 ms per panel (hidden
-// behind a wide trailing SYRK), so narrow strips keep the per-block form.
-__global__ void sqinv_kernel(const double* __restrict__ U, size_t ldu, int n, int nb2, int p0,
-                             const double* __restrict__ winv, double* __restrict__ sqinv);
-
-static int factor_panel_inv(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
-  constexpr int NB = 128;
-  const int nb = ctx->nb, nb2 = std::max(nb, (ctx->nb2 / nb) * nb);
-  const int kend = k + kw, nrest = n - kend;
-  GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap,
-                     (size_t)((n + nb2 - 1) / nb2) * nb2 * nb2));
-  for (int j = k; j < kend; j += nb) {
-    const int jb = std::min(nb, n - j);
-    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
-    GPR_TRY(launch_diag(ctx, A, lda, n, j, wj, 1, 1));
-    const int c1 = j + jb;
-    if (c1 >= kend) break;
-    double* row = A + j + (size_t)c1 * lda;
-    GemmArgs g{};
-    g.P = wj; g.ldp = nb;
-    g.Q = row; g.ldq = lda;
-    g.C = row; g.ldc = lda;
-    g.M = jb; g.N = kend - c1; g.K = jb;
-    g.alpha = 1.0; g.beta = 0.0;
-    g.info = ctx->dinfo;
-    GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
-    GemmArgs u{};
-    u.P = row; u.ldp = lda;
-    u.Q = row; u.ldq = lda;
-    u.C = A + c1 + (size_t)c1 * lda; u.ldc = lda;
-    u.M = kend - c1; u.N = kend - c1; u.K = jb;
-    u.alpha = -1.0; u.beta = 1.0;
-    u.upper = 1;
-    u.info = ctx->dinfo;
-    GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
-  }
-  double* sq = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2;
-  {
-    TimerScope ts(ctx, TC_PANEL, 0.0);
-    sqinv_kernel<<<dim3(1, (kw + NB - 1) / NB), 256, 0, ctx->ls>>>(A, (size_t)lda, n, nb2,
-                                                                   k / nb2, ctx->winv,
-                                                                   ctx->dsqinv);
-    LAUNCH_CHECK(ctx);
-  }
-  GPR_TRY(ensure_buf(ctx, &ctx->dpanel, &ctx->panel_cap, (size_t)kw * nrest));
-  GemmArgs g{};
-  g.P = sq; g.ldp = kw;                                  // U_sq^{-1}, upper triangular
-  g.Q = A + k + (size_t)kend * lda; g.ldq = lda;         // rows [k, kend) right of the square
-  g.C = ctx->dpanel; g.ldc = kw;                         // out of place: tiles share Q columns
-  g.M = kw; g.N = nrest; g.K = kw;
-  g.alpha = 1.0; g.beta = 0.0;
-  g.kend_from_m = 1;
-  g.info = ctx->dinfo;
-  GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
-  HIP_TRY(ctx, hipMemcpy2DAsync(A + k + (size_t)kend * lda, sizeof(double) * lda, ctx->dpanel,
-                                sizeof(double) * kw, sizeof(double) * kw, nrest,
-                                hipMemcpyDeviceToDevice, ctx->ls));
-  return 0;
-}
-
-// Recursive panel (GPR_PANEL=4): rows [k, k+kw) factored by halves -- the left half of the
-// panel rows recursively (its row TRSMs full width), then ONE update of the right half's rows
-// over all columns right of them with K = kw/2, then the right half.  Same flops and the same
-// chain of diagonal blocks as the per-block loop, but the in-panel updates run at K = 512,
-// 256, 128 (half, a quarter, a quarter of the work) instead of all at K = 128, so the panel
-// stream takes less CU time from the trailing SYRK it overlaps.
-static int factor_panel_rec(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
-  const int nb = ctx->nb;
-  if (kw <= nb) {
-    const int jb = std::min(nb, n - k);
-    double* wj = ctx->winv + (size_t)(k / nb) * nb * nb;
-    GPR_TRY(launch_diag(ctx, A, lda, n, k, wj, 1, 1));
-    if (k + jb >= n) return 0;
-    double* row = A + k + (size_t)(k + jb) * lda;
-    GemmArgs g{};
-    g.P = wj; g.ldp = nb;
-    g.Q = row; g.ldq = lda;
-    g.C = row; g.ldc = lda;
-    g.M = jb; g.N = n - k - jb; g.K = jb;
-    g.alpha = 1.0; g.beta = 0.0;
-    g.info = ctx->dinfo;
-    return launch_gemm_tn(ctx, g, TC_PANEL);
-  }
-  const int h = ((kw / nb + 1) / 2) * nb;  // left half, whole blocks
-  GPR_TRY(factor_panel_rec(ctx, A, n, lda, k, h));
-  const int r0 = k + h, rows = kw - h;
-  if (rows <= 0 || r0 >= n) return 0;
-  GemmArgs u{};
-  u.P = A + k + (size_t)r0 * lda; u.ldp = lda;   // U(k:k+h, r0:r0+rows)
-  u.Q = u.P; u.ldq = lda;                         // U(k:k+h, r0:n)
-  u.C = A + r0 + (size_t)r0 * lda; u.ldc = lda;
-  u.M = rows; u.N = n - r0; u.K = h;
-  u.alpha = -1.0; u.beta = 1.0;
-  u.mask_upper = 1;
-  u.info = ctx->dinfo;
-  GPR_TRY(launch_gemm_tn(ctx, u, TC_PANEL));
-  return factor_panel_rec(ctx, A, n, lda, r0, rows);
-}
-
-// Block lookahead (GPR_INNER_LA=2): the chain stream carries only what the next diagonal
-// block needs -- diag(j), the row TRSM of block j's NEXT nb columns, the update of the next
-// diagonal block -- and the full-width rest of step j (row TRSM of the far columns, update
-// of the far part of the panel) runs on stream3 beside diag(j+1).  The chain waits for step
-// j-1's far update before step j's near TRSM (that update wrote block (j, j+1) and, through
-// the panel rows, block (j+1, j+1)).
-static int factor_panel_bla(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
-  const int nb = ctx->nb;
-  hipStream_t home = ctx->ls, side = ctx->stream3;
-  hipEvent_t e_far = nullptr;  // far update of the previous step (on side)
-  int rc = 0;
-  auto gemm_on = [&](hipStream_t s, GemmArgs& g) {
-    ctx->ls = s;
-    const int r = launch_gemm_tn(ctx, g, TC_PANEL);
-    ctx->ls = home;
-    return r;
-  };
-  for (int j = k; j < k + kw && !rc; j += nb) {
-    const int jb = std::min(nb, n - j);
-    double* wj = ctx->winv + (size_t)(j / nb) * nb * nb;
-    if ((rc = launch_diag(ctx, A, lda, n, j, wj, 1, 1))) break;
-    if (j + jb >= n) break;
-    const int c1 = j + jb;                  // first column right of block j
-    const int jn = std::min(nb, n - c1);    // width of the next block
-    const int cf = c1 + jn;                 // first far column
-    const int pend = k + kw;                // end of this panel's rows
-    double* row = A + j + (size_t)c1 * lda;  // U_j, columns c1..n
-    hipEvent_t e_d = sync_event(ctx, ctx->ev_next++);
-    HIP_TRY(ctx, hipEventRecord(e_d, home));
-    // ---- chain: near row TRSM (after the previous far update), near diagonal update
-    if (e_far) HIP_TRY(ctx, hipStreamWaitEvent(home, e_far, 0));
-    e_far = nullptr;
-    GemmArgs sn{};
-    sn.P = wj; sn.ldp = nb;
-    sn.Q = row; sn.ldq = lda;
-    sn.C = row; sn.ldc = lda;
-    sn.M = jb; sn.N = jn; sn.K = jb;
-    sn.alpha = 1.0; sn.beta = 0.0;
-    sn.info = ctx->dinfo;
-    if ((rc = gemm_on(home, sn))) break;
-    hipEvent_t e_sn = sync_event(ctx, ctx->ev_next++);
-    HIP_TRY(ctx, hipEventRecord(e_sn, home));
-    if (pend > c1) {
-      GemmArgs un{};
-      un.P = row; un.ldp = lda;
-      un.Q = row; un.ldq = lda;
-      un.C = A + c1 + (size_t)c1 * lda; un.ldc = lda;
-      un.M = jn; un.N = jn; un.K = jb;
-      un.alpha = -1.0; un.beta = 1.0;
-      un.mask_upper = 1;
-      un.info = ctx->dinfo;
-      if ((rc = gemm_on(home, un))) break;
-    }
-    if (cf >= n) continue;  // no far columns: nothing for the side stream
-    // ---- side: far row TRSM, then the far update of the panel rows below block j
-    HIP_TRY(ctx, hipStreamWaitEvent(side, e_d, 0));
-    GemmArgs sf{};
-    sf.P = wj; sf.ldp = nb;
-    sf.Q = A + j + (size_t)cf * lda; sf.ldq = lda;
-    sf.C = A + j + (size_t)cf * lda; sf.ldc = lda;
-    sf.M = jb; sf.N = n - cf; sf.K = jb;
-    sf.alpha = 1.0; sf.beta = 0.0;
-    sf.info = ctx->dinfo;
-    if ((rc = gemm_on(side, sf))) break;
-    if (pend > c1) {
-      HIP_TRY(ctx, hipStreamWaitEvent(side, e_sn, 0));
-      GemmArgs fi{};  // rows of block j+1, far columns
-      fi.P = row; fi.ldp = lda;
-      fi.Q = A + j + (size_t)cf * lda; fi.ldq = lda;
-      fi.C = A + c1 + (size_t)cf * lda; fi.ldc = lda;
-      fi.M = jn; fi.N = n - cf; fi.K = jb;
-      fi.alpha = -1.0; fi.beta = 1.0;
-      fi.info = ctx->dinfo;
-      if ((rc = gemm_on(side, fi))) break;
-      if (pend > cf) {  // the remaining panel rows, far columns (upper part)
-        GemmArgs fr{};
-        fr.P = A + j + (size_t)cf * lda; fr.ldp = lda;
-        fr.Q = fr.P; fr.ldq = lda;
-        fr.C = A + cf + (size_t)cf * lda; fr.ldc = lda;
-        fr.M = pend - cf; fr.N = n - cf; fr.K = jb;
-        fr.alpha = -1.0; fr.beta = 1.0;
-        fr.mask_upper = 1;
-        fr.info = ctx->dinfo;
-        if ((rc = gemm_on(side, fr))) break;
-      }
-    }
-    e_far = sync_event(ctx, ctx->ev_next++);
-    HIP_TRY(ctx, hipEventRecord(e_far, side));
-  }
-  ctx->ls = home;
-  if (e_far) HIP_TRY(ctx, hipStreamWaitEvent(home, e_far, 0));  // panel complete on home
-  return rc;
 }
 
 // All outer-panel square inverses U_sq^{-1} of a finished factor in one launch: grid
@@ -1481,41 +1031,6 @@ __global__ __launch_bounds__(256) void colnorm_sub_kernel(const double* __restri
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if (lane == 0) norm[j] -= s;
-}
-
-// Outer panel rows [k, k+kw) by the square kernel + one GEMM (see square_panel_kernel).
-// U_sq^{-1} of panel k / nb2 is kept in ctx->dsqinv for the solves.
-int factor_panel_sq(gpr_ctx* ctx, double* A, int n, int lda, int k, int kw) {
-  constexpr int NB = 128;
-  const int nb2 = std::max(NB, (ctx->nb2 / NB) * NB);   // as potrf_core
-  const int nsq = (kw + NB - 1) / NB;
-  const size_t slots = (size_t)((n + nb2 - 1) / nb2);
-  GPR_TRY(ensure_buf(ctx, &ctx->dsqinv, &ctx->sqinv_cap, slots * nb2 * nb2));
-  if (!ctx->dsync) HIP_TRY(ctx, hipMalloc((void**)&ctx->dsync, 4096));
-  double* sq = ctx->dsqinv + (size_t)(k / nb2) * nb2 * nb2;
-  HIP_TRY(ctx, hipMemsetAsync(ctx->dsync, 0, sizeof(int) * (nsq + 1), ctx->ls));
-  {
-    TimerScope ts(ctx, TC_PANEL, 0.0);
-    square_panel_kernel<<<nsq, 256, 0, ctx->ls>>>(A, (size_t)lda, n, k, kw, ctx->winv, sq,
-                                                   ctx->dinfo, ctx->dsync);
-    LAUNCH_CHECK(ctx);
-  }
-  const int nrest = n - k - kw;
-  if (nrest <= 0) return 0;
-  GPR_TRY(ensure_buf(ctx, &ctx->dpanel, &ctx->panel_cap, (size_t)kw * nrest));
-  GemmArgs g{};
-  g.P = sq; g.ldp = kw;                                  // U_sq^{-1}, upper triangular
-  g.Q = A + k + (size_t)(k + kw) * lda; g.ldq = lda;     // rows [k, k+kw) right of the square
-  g.C = ctx->dpanel; g.ldc = kw;                         // out of place: tiles share Q columns
-  g.M = kw; g.N = nrest; g.K = kw;
-  g.alpha = 1.0; g.beta = 0.0;
-  g.kend_from_m = 1;
-  g.info = ctx->dinfo;
-  GPR_TRY(launch_gemm_tn(ctx, g, TC_PANEL));
-  HIP_TRY(ctx, hipMemcpy2DAsync(A + k + (size_t)(k + kw) * lda, sizeof(double) * lda, ctx->dpanel,
-                                sizeof(double) * kw, sizeof(double) * kw, nrest,
-                                hipMemcpyDeviceToDevice, ctx->ls));
-  return 0;
 }
 
 // TRSM panel: X_j = W_j^T B_j for the inner blocks of rows [k, k+kw), each followed by
@@ -1691,11 +1206,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   if (rhs && rhs->gram)  // accumulated panel by panel below (upper; the caller mirrors)
     HIP_TRY(ctx, hipMemset2DAsync(rhs->gram, (size_t)rhs->ldg * sizeof(double), 0,
                                   (size_t)n * sizeof(double), n, user));
-  hipStream_t s0 = ctx->smain ? ctx->smain : ctx->stream, s1 = ctx->stream2;
-  // with fused right-hand sides the trailing updates may run on a high-priority stream so the
-  // (normal-priority) solve only takes CUs the factorisation leaves idle (GPR_RHS_LOWPRIO=1)
-  static const bool rhs_lowprio = getenv("GPR_RHS_LOWPRIO") && atoi(getenv("GPR_RHS_LOWPRIO"));
-  if (rhs && rhs_lowprio && ctx->stream3 && !ctx->inner_la) s0 = ctx->stream3;
+  hipStream_t s0 = ctx->stream, s1 = ctx->stream2;
   HIP_TRY(ctx, hipMemsetAsync(ctx->dinfo, 0, sizeof(int), user));
   size_t ev = 0;
   ctx->ev_next = 1000;  // events of the diag hops use a separate index range
@@ -1708,15 +1219,12 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   hipStream_t sr = !rhs ? nullptr : (rhs->mode == 2 ? s0 : ctx->srhs);
   if (sr && sr != s0) HIP_TRY(ctx, hipStreamWaitEvent(sr, e0, 0));
   ctx->ls = s1;
-  const bool sqp = ctx->panel_sq && nb == 128 && nb2 <= 2048;
-  auto panel = [&](int k, int kw) {
-    return sqp ? factor_panel_sq(ctx, dA, n, lda, k, kw) : factor_panel(ctx, dA, n, lda, k, kw);
-  };
+  auto panel = [&](int k, int kw) { return factor_panel(ctx, dA, n, lda, k, kw); };
   // outer block k of the right-hand sides once panel k of U is final (event ev_final)
   // U_sq^{-1} of outer panel k on ssq once the panel is final (off the solve's own chain);
   // the square path wrote it already
   auto sq_inverse = [&](int k, hipEvent_t ev_final) -> hipEvent_t {
-    if (!sr || sqp) return ev_final;
+    if (!sr) return ev_final;
     if (hipStreamWaitEvent(ctx->ssq, ev_final, 0) != hipSuccess) return nullptr;
     ctx->ls = ctx->ssq;
     {
@@ -1754,7 +1262,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   // tail hand-off: once the trailing matrix is <= dag_tail, ONE SYRK applies panel s to all of
   // it and the tile-DAG factors it (the blocked path is chain-bound there)
   const bool tail_ok = ctx->dag_tail > 0 && !rhs && nb == 128 && lda % 16 == 0 &&
-                       ((uintptr_t)dA & 127) == 0 && n % 16 == 0 && !sqp;
+                       ((uintptr_t)dA & 127) == 0 && n % 16 == 0;
   bool tail_done = false;
   for (int k = 0; !rc && k + nb2 < n; k += nb2) {
     const int kend = k + nb2, w2 = std::min(nb2, n - kend), rest0 = kend + w2;
@@ -1799,30 +1307,18 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
     ctx->ls = s0;
     if (hipStreamWaitEvent(s0, ev_p, 0) != hipSuccess) { rc = GPR_E_HIP; break; }
     if (rest0 < n) {
-      // b_s as `pieces` launches of ~equal work (column bands [c0, c1) of the upper
-      // trailing matrix), so the lookahead stream gets dispatch opportunities in between
+      // b_s: the upper trailing matrix in one launch (round 1's split into column bands, to
+      // give the lookahead stream dispatch slots in between, measured no faster)
       const int R = n - rest0;
-      const int pieces = std::max(1, std::min(ctx->syrk_pieces, R / 1024));
-      int c0 = 0;
-      for (int pi = 1; pi <= pieces && !rc; ++pi) {
-        int c1 = pi == pieces ? R : (int)(std::sqrt((double)pi / pieces) * R) / 128 * 128;
-        if (c1 <= c0) continue;
-        GemmArgs b{};
-        b.P = dA + k + (size_t)rest0 * lda; b.ldp = lda;   // rows [0, c1) of the band
-        b.Q = dA + k + (size_t)(rest0 + c0) * lda; b.ldq = lda;
-        b.C = dA + rest0 + (size_t)(rest0 + c0) * lda; b.ldc = lda;
-        b.M = c1; b.N = c1 - c0; b.K = nb2;
-        b.alpha = -1.0; b.beta = 1.0;
-        if (c0 == 0) {
-          b.upper = 1;
-        } else {
-          b.mask_upper = 1;
-          b.mask_off = c0;
-        }
-        b.info = ctx->dinfo;
-        rc = launch_gemm_tn(ctx, b, TC_SYRK);
-        c0 = c1;
-      }
+      GemmArgs b{};
+      b.P = dA + k + (size_t)rest0 * lda; b.ldp = lda;
+      b.Q = dA + k + (size_t)rest0 * lda; b.ldq = lda;
+      b.C = dA + rest0 + (size_t)rest0 * lda; b.ldc = lda;
+      b.M = R; b.N = R; b.K = nb2;
+      b.alpha = -1.0; b.beta = 1.0;
+      b.upper = 1;
+      b.info = ctx->dinfo;
+      rc = launch_gemm_tn(ctx, b, TC_SYRK);
       if (rc) break;
     }
     ev_b = sync_event(ctx, ev++);
@@ -1856,7 +1352,7 @@ int potrf_core(gpr_ctx* ctx, double* dA, int n, int lda, int* info, const RhsSpe
   if (tail_done && hinfo < 0)
     return set_err(ctx, GPR_E_HIP, "tile-DAG factorisation: a dependency wait timed out");
   if (info) *info = hinfo;
-  if (hinfo == 0 && (sqp || rhs)) {
+  if (hinfo == 0 && rhs) {
     ctx->sqinv_nb2 = nb2;
     ctx->sq_ptr = dA;
     ctx->sq_n = n;
@@ -1894,7 +1390,7 @@ int ensure_factor_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
 int ensure_sq_inverses(gpr_ctx* ctx, const double* dU, int n, int ldu) {
   constexpr int NB = 128;
   const int nb2 = std::max(NB, (ctx->nb2 / NB) * NB);
-  if (ctx->nb != NB || nb2 > 2048 || getenv("GPR_TRSM_LEGACY")) return 0;
+  if (ctx->nb != NB || nb2 > 2048) return 0;
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   if (ctx->sqinv_nb2 == nb2 && ctx->sq_ptr == dU && ctx->sq_n == n && ctx->sq_ld == ldu) return 1;
   const int np = (n + nb2 - 1) / nb2;
@@ -2066,7 +1562,7 @@ int potrs_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int n
   GPR_TRY(ensure_factor_inverses(ctx, dU, n, ldu));
   const int nb = ctx->nb;
   const int nblk = (n + nb - 1) / nb;
-  if (nb == SW_NB && !getenv("GPR_POTRS_LEGACY")) {
+  if (nb == SW_NB) {
     GPR_TRY(ensure_buf(ctx, &ctx->dtrsv, &ctx->trsv_cap, (size_t)n * 2));
     int* sync = ctx->dinfo + 4;  // dinfo[4..7]: fwd ticket/done, bwd ticket/done
     for (int c0 = 0; c0 < nrhs; c0 += 2) {

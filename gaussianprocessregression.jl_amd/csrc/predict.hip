@@ -506,10 +506,49 @@ static int ensure_children(gpr_ctx* ctx, int nsub) {
     if (ctx->cv_sub[t]) continue;
     const int rc = gpr_ctx_create(ctx->device, nullptr, &ctx->cv_sub[t]);
     if (rc) return set_err(ctx, rc, "creating a child context failed");
+  }
+  for (int t = 0; t < nsub; ++t) {  // (every call: the parent's settings may have changed)
     ctx->cv_sub[t]->nb = ctx->nb;
     ctx->cv_sub[t]->nb2 = ctx->nb2;
+    copy_knobs(ctx, ctx->cv_sub[t]);
   }
   return 0;
+}
+
+// Batch size of a batched launch: `want` items of `per` doubles each (+ `fixed`), within the
+// context's budget (GB) and half of the device memory free right now -- the buffer being
+// replaced (cap doubles, freed by ensure_buf first) counts as free.  At least one.
+static int batch_capacity(double budget_gb, size_t per, size_t fixed, size_t cap, int want) {
+  double bytes = budget_gb * 1e9;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+    bytes = std::min(bytes, 0.5 * (double)fr + 8.0 * (double)cap);
+  const double avail = bytes / 8.0 - (double)fixed;
+  const double k = avail > 0 ? avail / (double)per : 0.0;
+  return (int)std::max(1.0, std::min((double)want, std::floor(k)));
+}
+
+// A batched launch's workspace with its batch count halved on an allocation failure (another
+// allocator may hold memory hipMemGetInfo counted as free) down to one item; then GPR_E_NOMEM.
+static int ensure_batch_buf(gpr_ctx* ctx, int* nb, const std::function<size_t(int)>& need) {
+  for (;;) {
+    const int rc = ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, need(*nb));
+    if (rc != GPR_E_NOMEM || *nb <= 1) return rc;
+    (void)hipGetLastError();
+    ctx->err.clear();
+    *nb = (*nb + 1) / 2;
+  }
+}
+
+// The batched paths size ctx->dbig to their batch; past a call it is released again when
+// large, so a context does not keep gigabytes of scratch between calls.
+static void release_big_scratch(gpr_ctx* ctx) {
+  if (ctx->dbig && ctx->big_cap * sizeof(double) > (size_t)(1ull << 30)) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->dbig);
+    ctx->dbig = nullptr;
+    ctx->big_cap = 0;
+  }
 }
 
 // Cap the number of child contexts so their workspaces (bytes_each, allocated in each child's
@@ -647,18 +686,24 @@ __global__ void pad_identity_kernel(double* __restrict__ A, size_t lda, size_t s
 // Sigma_f = K(x_ts, x_ts) (padded to s2); the launch leaves V_f = U_f^{-T} W_f, then mu =
 // V_kx^T v_y, Sigma_p = Sigma_f - V_kx^T V_kx (upper triangle), and the loss -- gpr_fit_predict's
 // FULL path per fold with its chain-bound factorisations batched ("cv needs batched
-// small POTRFs").  Returns > 0 as the sequential path does (a fold's info), 0 when done.
+// small POTRFs").  Returns > 0 as the sequential path does (a fold's info), 0 when done; 1 with
+// *declined set when the batched launch does not take the shape (nothing written: the shape
+// is the same for every chunk, so only the first launch can decline).
 static int cv_folds_batched(gpr_ctx* ctx, const KParams& kp, int d, const double* dX, int n,
                             const double* dy, const int* trn, int ntrn, const int* tst, int ntst,
-                            int nfold, int cost, double* lss) {
+                            int nfold, int cost, double* lss, bool* declined) {
+  *declined = false;
   const int n2 = (ntrn + 15) / 16 * 16, s2 = (ntst + 15) / 16 * 16;
   const size_t szK = (size_t)n2 * n2, szW = (size_t)n2 * (ntst + 1), szS = (size_t)s2 * s2;
   const size_t per = szK + szW + szS + 2 * (size_t)s2 + 1;
-  const double budget = getenv("GPR_CV_BATCH_GB") ? atof(getenv("GPR_CV_BATCH_GB")) : 16.0;
-  const int nfc = (int)std::max<size_t>(1, std::min<size_t>((size_t)nfold, (size_t)(budget * 1e9 / 8.0) / per));
   const size_t scratch = (size_t)d * (ntrn + ntst) + ntrn;
+  auto need = [&](int k) {
+    return per * k + scratch + ((size_t)k * (ntrn + ntst) + 1) / 2 + 16;
+  };
+  int nfc = batch_capacity(ctx->cv_batch_gb, per + (ntrn + ntst + 1) / 2, scratch + 16,
+                           ctx->big_cap, nfold);
+  GPR_TRY(ensure_batch_buf(ctx, &nfc, need));
   const size_t nidx = (size_t)nfc * (ntrn + ntst);
-  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per * nfc + scratch + (nidx + 1) / 2 + 16));
   double* Kb = ctx->dbig;                 // nfc x szK
   double* Wb = Kb + szK * nfc;            // nfc x szW
   double* Sb = Wb + szW * nfc;            // nfc x szS
@@ -711,6 +756,10 @@ static int cv_folds_batched(gpr_ctx* ctx, const KParams& kp, int d, const double
       LAUNCH_CHECK(ctx);
     }
     int rc = launch_potrf_dag_batch(ctx, Kb, szK, n2, n2, Wb, szW, ntst + 1, n2, nb, info.data());
+    if (rc == 1 && f0 == 0) {
+      *declined = true;
+      return 1;
+    }
     if (rc) return rc == 1 ? set_err(ctx, GPR_E_HIP, "batched cross-validation: shape declined") : rc;
     for (int i = 0; i < nb; ++i)
       if (info[i] > 0) return info[i];
@@ -736,6 +785,10 @@ static int cv_folds_batched(gpr_ctx* ctx, const KParams& kp, int d, const double
     if (cost == GPR_COST_MAHALANOBIS) {
       // delta = y - yp; Sigma_p = U^T U; ||U^{-T} delta||^2 (:25-30) -- the second batch
       rc = launch_potrf_dag_batch(ctx, Sb, szS, s2, s2, Yp, (size_t)s2, 1, s2, nb, info.data());
+      if (rc == 1 && f0 == 0) {
+        *declined = true;
+        return 1;
+      }
       if (rc) return rc == 1 ? set_err(ctx, GPR_E_HIP, "batched cross-validation: shape declined") : rc;
       for (int i = 0; i < nb; ++i)
         if (info[i] > 0) return info[i];
@@ -770,9 +823,16 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
         return set_err(ctx, GPR_E_ARG, "test index out of range");
   }
   // Every fold's factorisation in one batched tile-DAG launch (default; GPR_CV_BATCH=0: the
-  // per-fold path below, folds spread over child contexts -- 1.1-2.7x slower, tools/bench_cv.py)
-  if (!getenv("GPR_CV_BATCH") || atoi(getenv("GPR_CV_BATCH")) != 0)
-    return cv_folds_batched(ctx, kp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, cost, lss);
+  // per-fold path below, folds spread over child contexts -- 1.1-2.7x slower, tools/bench_cv.py;
+  // also taken when the batched launch declines the shape)
+  if (ctx->cv_batch) {
+    bool declined = false;
+    const int rc = cv_folds_batched(ctx, kp, d, dX, n, dy, trn, ntrn, tst, ntst, nfold, cost, lss,
+                                    &declined);
+    release_big_scratch(ctx);
+    if (!declined) return rc;
+    ctx->err.clear();
+  }
   // A fold below ~8k training points is a latency-bound chain of small launches (diag
   // block, panel GEMM, update per 128 columns) that leaves most CUs idle, so independent
   // folds run concurrently, one child context (own streams, own workspace) per host thread.
@@ -896,9 +956,8 @@ static int integ_noise_batched(gpr_ctx* ctx, const double* K, int n, const doubl
   *declined = false;
   const int n2 = (n + 15) / 16 * 16;
   const size_t per = (size_t)n2 * n2 + 2 * (size_t)n2;
-  const double budget = getenv("GPR_QUAD_BATCH_GB") ? atof(getenv("GPR_QUAD_BATCH_GB")) : 16.0;
-  const int nbc = (int)std::max<size_t>(1, std::min<size_t>((size_t)ny, (size_t)(budget * 1e9 / 8.0) / per));
-  GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, per * nbc + (size_t)3 * nbc + 16));
+  int nbc = batch_capacity(ctx->quad_batch_gb, per + 3, 16, ctx->big_cap, ny);
+  GPR_TRY(ensure_batch_buf(ctx, &nbc, [&](int k) { return per * k + (size_t)3 * k + 16; }));
   double* W = ctx->dbig;
   double* Bm = W + (size_t)n2 * n2 * nbc;
   double* dnoise = Bm + (size_t)2 * n2 * nbc;
@@ -1127,8 +1186,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   // conservative), else the eigensolver; a batch that meets a non-positive-definite K + s I
   // (a shift at or below -lambda_min(K)) falls back to the eigensolver.  =1 forces the eigensolver, =0 the factorisations (GPR_QUAD_SEQ: one at a
   // time, as before the batched launch).
-  const char* qe = getenv("GPR_QUAD_EIGEN");
-  int qmode = qe ? atoi(qe) : -1;
+  int qmode = ctx->quad_eigen;
   bool fallback = false;
   if (qmode < 0) {
     // any shift: K + s I is positive definite for s >= 0 and for -lambda_min(K) < s < 0; a
@@ -1141,9 +1199,10 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
     const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode == 2);
     if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
   }
-  if (!getenv("GPR_QUAD_SEQ")) {  // the batched launch (GPR_QUAD_SEQ: one column at a time)
+  if (!ctx->quad_seq) {  // the batched launch (GPR_QUAD_SEQ: one column at a time)
     bool declined = false;
     const int rc = integ_noise_batched(ctx, K, n, dy, ldy, k1, k2, noise, ny, Iout, var, &declined);
+    release_big_scratch(ctx);
     if (!declined) {
       if (rc > 0 && fallback) {  // K + s I not numerically positive definite: the eigensolver
         ctx->err.clear();

@@ -56,6 +56,8 @@ _SIGS = {
     "gpr_download": (_i, [_p, _p, _p, c_size_t]),
     "gpr_set_block": (_i, [_p, _i]),
     "gpr_set_outer_block": (_i, [_p, _i]),
+    "gpr_set_knob": (_i, [_p, ctypes.c_char_p, _d]),
+    "gpr_get_knob": (_i, [_p, ctypes.c_char_p, _dp]),
     "gpr_timing_enable": (_i, [_p, _i]),
     "gpr_timing_get": (_i, [_p, _i, _dp, POINTER(c_longlong), _dp]),
     "gpr_timing_reset": (_i, [_p]),

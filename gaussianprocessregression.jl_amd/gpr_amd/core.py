@@ -42,6 +42,15 @@ class Context:
         if nb != 128:
             self.check(lib.gpr_set_block(self.h, nb))
 
+    def set_knob(self, name: str, value: float) -> None:
+        """gpr_set_knob: one of the library's documented switches (include/gpr_hip.h)."""
+        self.check(lib.gpr_set_knob(self.h, name.encode(), float(value)), f"set_knob({name})")
+
+    def get_knob(self, name: str) -> float:
+        v = ctypes.c_double()
+        self.check(lib.gpr_get_knob(self.h, name.encode(), ctypes.byref(v)), f"get_knob({name})")
+        return v.value
+
     def check(self, rc: int, what: str = "") -> int:
         if rc < 0:
             msg = lib.gpr_last_error(self.h).decode()

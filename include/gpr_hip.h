@@ -84,6 +84,37 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
  *        launches (with any right-hand sides they solve), 7 solve-only tile-DAG launches
  *        (U^{-T} B from a finished factor: C5's variance rows, POTRI's Z).
  *        Returns accumulated ms, launch count, flops (bytes for class 0). */
+/* Knobs: the library's run-time switches.  Each is a GPR_* environment variable read ONCE,
+ * when a context is created, and can be changed on a live context with gpr_set_knob (values
+ * are doubles, integer knobs truncate).  None of them changes a result beyond rounding: they
+ * pick between equivalent code paths or size workspaces.  Unknown names: GPR_E_ARG.
+ *   GPR_DAG            1  factorisations as one persistent tile-DAG launch; 0: the blocked
+ *                         two-stream factorisation (inner nb, outer nb2)
+ *   GPR_DAG_TAIL   12288  blocked path: the last <= this many columns go to the tile-DAG (0 off)
+ *   GPR_DAG_SOLVE     -1  solves from a finished factor as solve-only tile-DAG launches
+ *                         (-1 auto: n >= 8192 with >= n right-hand sides; 0 never; 1 always)
+ *   GPR_DAG_GRAM       1  gpr_fit_kinv: K^{-1} = Z^T Z as gram tasks of the DAG launch
+ *   GPR_DAG_ZLAG       4  DAG: Z = U^{-T}'s row i scheduled after A's row i + lag
+ *   GPR_FUSED_RHS     -1  gpr_fit_predict: [K(x, xp) | y] solved inside the factorisation
+ *                         (-1 auto, 0 after it, 1 own stream, 2 main stream; blocked path)
+ *   GPR_FUSE_Y         1  gpr_fit: z = U^{-T} y inside the factorisation
+ *   GPR_FUSE_KINV     -1  gpr_fit_kinv: Z (1) and Z^T Z (2) inside the factorisation (-1 = 2)
+ *   GPR_KBUILD_UPPER   1  fits assemble only what dpotrf 'U' reads (the DAG mirrors the rest)
+ *   GPR_KBUILD_EXACT   0  1: K by the reference's difference form instead of the Gram form
+ *   GPR_CV_BATCH       1  gpr_cv_batch: every fold in one batched launch; 0: per fold
+ *   GPR_CV_BATCH_GB   16  device-memory budget of one batched cross-validation launch
+ *   GPR_CV_STREAMS     4  child contexts of the per-fold / per-column paths (<= 8)
+ *   GPR_QUAD_EIGEN    -1  gpr_integrate_noise: -1 auto, 0 per-column factorisations,
+ *                         1 the eigensolver, 2 rocSOLVER dsyevd (timing comparator only)
+ *   GPR_QUAD_BATCH_GB 16  device-memory budget of one batched quadrature launch
+ *   GPR_QUAD_SEQ       0  1: the per-column factorisations one at a time (no batch)
+ * A gpr_mgpu handle reads GPR_MGPU_STREAM (-1 auto: stream U out during device 0's fit only
+ * for one device), GPR_MGPU_CHUNKS (16), GPR_MGPU_RESERVE_CU (8) and GPR_MGPU_SELF_BCAST (0;
+ * 1: a one-device handle runs the broadcast protocol to itself) once, at gpr_mgpu_create.
+ * Fault injection (forced wait timeouts, failed unpacks) exists only in the test build
+ * libgpr_hip_testing.so. */
+int gpr_set_knob(gpr_ctx_t ctx, const char* name, double value);
+int gpr_get_knob(gpr_ctx_t ctx, const char* name, double* value);
 int gpr_timing_enable(gpr_ctx_t ctx, int on);
 int gpr_timing_get(gpr_ctx_t ctx, int cls, double* ms, long long* launches, double* flops);
 int gpr_timing_reset(gpr_ctx_t ctx);
@@ -122,7 +153,7 @@ int gpr_kernel_grad(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, i
  * Implementation: one persistent tile-DAG launch (128 x 128 tile tasks); n and lda
  * multiples of 16 with a 128-B aligned dA are factored in place, other shapes on a padded
  * device copy (n rounded up to 16: an extra ~8 n^2 bytes of device memory, same result);
- * GPR_DAG=0 in the environment selects the blocked two-stream factorisation. */
+ * the knob GPR_DAG=0 selects the blocked two-stream factorisation. */
 int gpr_potrf_upper(gpr_ctx_t ctx, double* dA, int n, int lda, int* info);
 
 /* The context caches the factor's block inverses (and the outer squares' inverses) after a
@@ -261,7 +292,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
  * symmetric) = P diag(lam) P'; on return dlam[n] (device) holds the eigenvalues -- in no
  * particular order -- and dB (n x m, ld ldb, device) holds P' B, its rows in the order of
  * dlam.  Two-sided block Jacobi (32-wide blocks, parallel ordering), FP64; *sweeps (may be
- * NULL) = sweeps used.  GPR_E_HIP if it does not converge (GPR_EIG_MAX_SWEEPS, default 60). */
+ * NULL) = sweeps used.  GPR_E_HIP if it does not converge within 60 sweeps. */
 int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                    double* dlam, int* sweeps);
 

@@ -29,3 +29,41 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def knobs():
+    """Set library knobs (include/gpr_hip.h) on the default context for one test:
+    ``knobs("GPR_QUAD_EIGEN", 1)``; every changed knob gets its old value back afterwards.
+    (The library reads its GPR_* environment once per context, at creation.)"""
+    import gpr_amd as G
+    from gpr_amd import core
+    ctx = core.default_context()
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = ctx.get_knob(name)
+        ctx.set_knob(name, value)
+
+    yield set_
+    for name, value in saved.items():
+        ctx.set_knob(name, value)
+
+
+TESTING_LIB = os.path.join(PKG, "gpr_amd", "libgpr_hip_testing.so")
+
+
+def run_fault_scenario(name, *args, timeout=300):
+    """Run tests/fault_scenarios.py <name> in a child process on the test build of the library
+    (fault injection is compiled only into libgpr_hip_testing.so)."""
+    import subprocess
+    assert os.path.exists(TESTING_LIB), "build it: make -C gaussianprocessregression.jl_amd/csrc"
+    env = dict(os.environ, GPR_HIP_LIB=TESTING_LIB)
+    for k in ("GPR_DAG_SPIN_LIMIT", "GPR_MGPU_GATE_LIMIT", "GPR_MGPU_FAIL_UNPACK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "fault_scenarios.py"), name,
+                        *map(str, args)], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0 and "OK" in r.stdout, \
+        f"scenario {name}{args} failed (rc {r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"

@@ -1,0 +1,135 @@
+"""Fault-injection scenarios for the GPU suite, run in a CHILD process against the test build
+of the library, libgpr_hip_testing.so (GPR_HIP_LIB; Makefile target $(TOUT), -DGPR_TESTING).
+The release libgpr_hip.so has no fault injection at all, so an inherited environment can
+never make it time out or drop a chunk on purpose; these scenarios need the switches the test
+build reads at call time: GPR_DAG_SPIN_LIMIT (every tile-DAG dependency wait gives up at once),
+GPR_MGPU_GATE_LIMIT (a streamed broadcast chunk's gate gives up), GPR_MGPU_FAIL_UNPACK (a
+receiver's unpack of chunk k fails).
+
+    python tests/fault_scenarios.py <scenario> [args...]   -> prints "OK" on success
+
+Each scenario checks that the fault is reported as an error (no hang, no wrong answer) and
+that the same context / handle gives correct results afterwards.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (HERE, ROOT, os.path.join(ROOT, "gaussianprocessregression.jl_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from oracle import gpr_oracle as O  # noqa: E402  (the checker)
+
+
+def dag_timeout():
+    """Every tile-DAG dependency wait is bounded (dag.hip dag_wait); GPR_DAG_SPIN_LIMIT=1
+    forces the bound to expire.  The launch must drain (no hang), the call must return
+    GPR_E_HIP with the timeout message -- the factorisation (gpr_fit_predict) and a solve-only
+    launch (gpr_potri_upper's Z) alike -- and the SAME context must give correct results once
+    the bound is back: the info flag a timed-out launch leaves behind must not make the next
+    solve-only launch skip its tasks."""
+    import gpr_amd as G
+    from test_gpu_parity import _dev_potrf, _spd, cov_of, relnorm
+    os.environ.pop("GPR_DAG_SPIN_LIMIT", None)
+    ctx = G.Context(0)
+    ctx.set_knob("GPR_DAG_SOLVE", 1)  # the solve-only tile-DAG at this size
+    n = 1024
+    A = _spd(n, seed=3)
+    dA, info = _dev_potrf(ctx, A)
+    assert info == 0
+    dK = ctx.empty(n, n)
+    potri = lambda: G._lib.lib.gpr_potri_upper(ctx.h, ctypes.c_void_p(dA.data_ptr()), n, n,  # noqa: E731
+                                               ctypes.c_void_p(dK.data_ptr()), n)
+    x, y, xp = O.synthetic(4, 1024, 200, seed_train=5)
+    kinds = [O.SE, O.WN]
+    hp = O.default_hp(kinds, 4)
+    md = G.GPRModel(cov_of(kinds), hp, x, y, ctx=ctx)
+    os.environ["GPR_DAG_SPIN_LIMIT"] = "1"
+    for _ in range(2):  # (twice: a drained launch leaves the context usable for the next one)
+        try:
+            G.predict(md, xp, diagonal_var=True)
+            raise AssertionError("no timeout reported")
+        except G.GprError as e:
+            assert "timed out" in str(e), e
+        assert potri() == -2
+        assert b"timed out" in G._lib.lib.gpr_last_error(ctx.h)
+    del os.environ["GPR_DAG_SPIN_LIMIT"]
+    # the factor in dA is intact (the timed-out launches were solves / other buffers); the
+    # solve-only launch right after a timed-out one on the same cached factor
+    assert potri() == 0
+    assert relnorm(ctx.host(dK), np.linalg.inv(A)) < 1e-11
+    mu, var = G.predict(md, xp, diagonal_var=True)
+    mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
+    np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-8 * O.diag_prior(kinds, hp, 4))
+
+
+def _mgpu_case(seed):
+    import gpr_amd as G
+    import gpr_amd.distributed as gd
+    from test_distributed import _problem
+    os.environ["GPR_MGPU_SELF_BCAST"] = "1"
+    kinds, hp, x, y, xe, xq = _problem(ne=7, nq=9, ns=4096, d=5, seed=seed)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    return G, gd, md, cm
+
+
+def _check_vs_single(G, md, cm, mu, var):
+    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 7))
+    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+
+
+def mgpu_gate_timeout():
+    """A streamed chunk whose gate gives up (GPR_MGPU_GATE_LIMIT=0: every gate at its first
+    poll) is reported as an error after every stream drained -- no hang -- and the next call on
+    the same handle, with the default limit, is correct."""
+    os.environ["GPR_MGPU_STREAM"] = "1"
+    G, gd, md, cm = _mgpu_case(13)
+    mg = gd.MultiGPU([0])
+    try:
+        os.environ["GPR_MGPU_GATE_LIMIT"] = "0"
+        try:
+            gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
+            raise AssertionError("no gate timeout reported")
+        except G.GprError as e:
+            assert "gate timed out" in str(e), e
+        del os.environ["GPR_MGPU_GATE_LIMIT"]
+        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
+    finally:
+        mg.close()
+    _check_vs_single(G, md, cm, mu, var)
+
+
+def mgpu_unpack_failure(stream, chunk):
+    """A receiver whose unpack of one chunk fails (GPR_MGPU_FAIL_UNPACK=k) keeps receiving
+    every remaining chunk and wt -- the sender posts them all -- and reports the error once the
+    protocol is complete: the call returns an error instead of hanging, and the next call on the
+    same handle is correct."""
+    os.environ["GPR_MGPU_STREAM"] = stream
+    os.environ["GPR_MGPU_CHUNKS"] = "5"
+    G, gd, md, cm = _mgpu_case(14)
+    mg = gd.MultiGPU([0])
+    try:
+        os.environ["GPR_MGPU_FAIL_UNPACK"] = chunk
+        try:
+            gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
+            raise AssertionError("no unpack failure reported")
+        except G.GprError as e:
+            assert f"unpack of chunk {chunk} failed" in str(e), e
+        del os.environ["GPR_MGPU_FAIL_UNPACK"]
+        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
+    finally:
+        mg.close()
+    _check_vs_single(G, md, cm, mu, var)
+
+
+if __name__ == "__main__":
+    globals()[sys.argv[1]](*sys.argv[2:])
+    print("OK", flush=True)

@@ -127,7 +127,7 @@ def test_cv_concurrent_folds_bit_identical(monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cname", ["MSE", "ChiSq", "Mahalanobis"])
-def test_cv_batched_launch_vs_per_fold(cname, monkeypatch):
+def test_cv_batched_launch_vs_per_fold(cname, knobs):
     """Every fold's factorisation (and, for Mahalanobis, every Sigma_p's) in one batched tile-DAG
     launch (GPR_CV_BATCH=1; padded to multiples of 16: ntrn = 341, ntst = 31 here) against the
     per-fold path: the same losses to rounding; a one-fold memory budget (one launch per fold)
@@ -137,13 +137,34 @@ def test_cv_batched_launch_vs_per_fold(cname, monkeypatch):
     hp = O.default_hp(["SE", "WN"], d, length=2.0)
     md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
     cvset = G.kfoldcv(n, k, rng=np.random.default_rng(4))
-    monkeypatch.setenv("GPR_CV_BATCH", "0")
+    knobs("GPR_CV_BATCH", 0)
     seq = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
-    monkeypatch.setenv("GPR_CV_BATCH", "1")
+    knobs("GPR_CV_BATCH", 1)
     bat = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
     np.testing.assert_allclose(bat, seq, rtol=1e-9, atol=0)
-    monkeypatch.setenv("GPR_CV_BATCH_GB", "1e-9")
+    knobs("GPR_CV_BATCH_GB", 1e-9)
     one = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
     np.testing.assert_array_equal(one, bat)
     want = O.cv_batch(["SE", "WN"], hp, cname, x, y, cvset)
     np.testing.assert_allclose(bat, want, rtol=1e-8, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cname", ["MSE", "Mahalanobis"])
+def test_cv_batch_context_nb64(cname):
+    """A context with 64-wide inner blocks (gpr_set_block) still takes the batched launch (its
+    tiles are 128 wide whatever the context's nb) and gives the oracle's losses; the per-fold
+    path of the same context agrees."""
+    d, n, k = 3, 300, 25
+    x, y = _data(d, n, 31)
+    hp = O.default_hp(["SE", "WN"], d, length=2.0)
+    cvset = G.kfoldcv(n, k, rng=np.random.default_rng(6))
+    ctx = G.Context(0, nb=64)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y, ctx=ctx)
+    bat = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
+    ctx.set_knob("GPR_CV_BATCH", 0)
+    seq = G.cv_batch(md, _COSTS[cname](), x, y, cvset)
+    ctx.close()
+    want = O.cv_batch(["SE", "WN"], hp, cname, x, y, cvset)
+    np.testing.assert_allclose(bat, want, rtol=1e-8, atol=0)
+    np.testing.assert_allclose(seq, bat, rtol=1e-9, atol=0)

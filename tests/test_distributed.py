@@ -520,56 +520,22 @@ def test_split_predict_shard_compact_equals_rows():
 
 
 @pytest.mark.gpu
-def test_split_predict_mgpu_gate_timeout_reports_and_recovers(monkeypatch):
-    """A streamed chunk whose gate gives up (GPR_MGPU_GATE_LIMIT=0: every gate at its first
-    poll) is reported as an error after every stream drained -- no hang -- and the next call on
-    the same handle, with the default limit, is correct."""
-    G = pytest.importorskip("gpr_amd")
-    monkeypatch.setenv("GPR_MGPU_SELF_BCAST", "1")
-    monkeypatch.setenv("GPR_MGPU_STREAM", "1")
-    kinds, hp, x, y, xe, xq = _problem(ne=7, nq=9, ns=4096, d=5, seed=13)
-    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
-    cm = G.Cmap("+", xe, xq)
-    mg = gd.MultiGPU([0])
-    try:
-        monkeypatch.setenv("GPR_MGPU_GATE_LIMIT", "0")
-        with pytest.raises(G.GprError, match="gate timed out"):
-            gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
-        monkeypatch.delenv("GPR_MGPU_GATE_LIMIT")
-        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
-    finally:
-        mg.close()
-    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 7))
-    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
-    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+def test_split_predict_mgpu_gate_timeout_reports_and_recovers():
+    """A streamed chunk whose gate gives up is reported as an error after every stream drained
+    -- no hang -- and the next call on the same handle is correct (fault_scenarios.py, child
+    process on the test build libgpr_hip_testing.so)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("mgpu_gate_timeout")
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream,chunk", [("1", "0"), ("1", "3"), ("0", "2")])
-def test_split_predict_mgpu_unpack_failure_reports_and_recovers(monkeypatch, stream, chunk):
-    """A receiver whose unpack of one chunk fails (GPR_MGPU_FAIL_UNPACK=k, fault injection the
-    self-broadcast receiver honours) keeps receiving every remaining chunk and wt -- the sender
-    posts them all -- and reports the error once the protocol is complete: the call returns an
-    error instead of hanging, and the next call on the same handle is correct."""
-    G = pytest.importorskip("gpr_amd")
-    monkeypatch.setenv("GPR_MGPU_SELF_BCAST", "1")
-    monkeypatch.setenv("GPR_MGPU_STREAM", stream)
-    monkeypatch.setenv("GPR_MGPU_CHUNKS", "5")
-    kinds, hp, x, y, xe, xq = _problem(ne=7, nq=9, ns=4096, d=5, seed=14)
-    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
-    cm = G.Cmap("+", xe, xq)
-    mg = gd.MultiGPU([0])
-    try:
-        monkeypatch.setenv("GPR_MGPU_FAIL_UNPACK", chunk)
-        with pytest.raises(G.GprError, match=f"unpack of chunk {chunk} failed"):
-            gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
-        monkeypatch.delenv("GPR_MGPU_FAIL_UNPACK")
-        mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 7), fit="broadcast")
-    finally:
-        mg.close()
-    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 7))
-    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
-    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
+def test_split_predict_mgpu_unpack_failure_reports_and_recovers(stream, chunk):
+    """A receiver whose unpack of one chunk fails keeps receiving every remaining chunk and wt
+    and reports the error once the protocol is complete; the next call on the same handle is
+    correct (fault_scenarios.py, child process on the test build libgpr_hip_testing.so)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("mgpu_unpack_failure", stream, chunk)
 
 
 @pytest.mark.gpu

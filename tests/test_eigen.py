@@ -99,12 +99,12 @@ def test_syev_diagonal_and_zero():
 
 
 @pytest.mark.parametrize("quad", ["1", "auto"])
-def test_integrate_noise_native_vs_rocsolver_comparator(quad, monkeypatch):
+def test_integrate_noise_native_vs_rocsolver_comparator(quad, knobs):
     """The hand-written eigensolver (GPR_QUAD_EIGEN=1) and the default (here the batched
     factorisations: every shift above -lambda_min) against rocSOLVER's dsyevd as a comparator
     (GPR_QUAD_EIGEN=2, timing/cross-check only) and against the oracle's eigen path."""
     if quad != "auto":
-        monkeypatch.setenv("GPR_QUAD_EIGEN", quad)
+        knobs("GPR_QUAD_EIGEN", int(quad))
     dim, n, ne = 3, 600, 6
     kinds = [O.SE, O.WN]
     rng = np.random.default_rng(9)
@@ -118,7 +118,7 @@ def test_integrate_noise_native_vs_rocsolver_comparator(quad, monkeypatch):
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
     np.testing.assert_allclose(I, Io, rtol=1e-8)
     np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
-    monkeypatch.setenv("GPR_QUAD_EIGEN", "2")
+    knobs("GPR_QUAD_EIGEN", 2)
     I2, v2 = G.integrate(md, a, b, sample_noise=noise)
     np.testing.assert_allclose(I2, I, rtol=1e-8)
     np.testing.assert_allclose(v2, v, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))

@@ -118,3 +118,39 @@ def test_c5_split_predict_vs_oracle_fixture():
     np.testing.assert_allclose(var[(lo - 1) * nq:hi * nq], fx["var_head"], rtol=1e-8,
                                atol=1e-8 * prior)
     assert np.all(var[hi * nq:] == prior)  # rows outside var_range keep the prior
+
+
+@pytest.mark.parametrize("stream", ["0", "1"])
+def test_c5_split_predict_mgpu_all_devices_vs_oracle_fixture(stream, monkeypatch):
+    """C5 sharded over EVERY visible device (gpr_split_predict_mgpu: one context and RCCL
+    communicator per device, cost-balanced e-row shards, rows copied straight into the host
+    result) against the oracle fixture -- the same rows and tolerances as the single-device
+    test above -- for both fit modes (device 0 fits and broadcasts the packed factor over
+    RCCL / every device fits) and both broadcast schedules (GPR_MGPU_STREAM: after the fit, or
+    streamed while device 0 factors).  Skips below two devices (the development pool has one
+    GPU per box; the driver's multi-GPU node runs it)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("needs two or more GPUs")
+    import gpr_amd.distributed as gd
+    monkeypatch.setenv("GPR_MGPU_STREAM", stream)  # (read at gpr_mgpu_create)
+    cfg, inp, fx = _load("C5")
+    kinds, hp = cfg["kinds"], inp["hp"]
+    md = G.GPRModel(_cov(kinds), hp, inp["x"], inp["y"])
+    cm = G.Cmap("+", inp["xe"], inp["xq"])
+    prior = O.diag_prior(kinds, hp, cfg["d"])
+    lo, hi = cfg["var_range"]
+    nq = cfg["nq"]
+    rows = fx["rows"]
+    mg = gd.MultiGPU(list(range(ndev)))
+    try:
+        for fit in ("broadcast", "replicate"):
+            mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=cfg["var_range"], fit=fit)
+            np.testing.assert_allclose(mu[rows], fx["mu_rows"], rtol=1e-8, atol=1e-10)
+            assert _relnorm(mu[rows], fx["mu_rows"]) <= 1e-8
+            np.testing.assert_allclose(var[(lo - 1) * nq:hi * nq], fx["var_head"], rtol=1e-8,
+                                       atol=1e-8 * prior)
+            assert np.all(var[hi * nq:] == prior)
+    finally:
+        mg.close()

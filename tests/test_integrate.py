@@ -124,11 +124,11 @@ def test_inverse_diagonal_update_oracle(n):
 @pytest.mark.parametrize("quad", ["auto", "1"])
 @pytest.mark.parametrize("name,dim,n,ne", [("SE", 2, 150, 7), ("SE+WN", 3, 300, 12),
                                            ("SE", 4, 1100, 5)])
-def test_integrate_sample_noise_vs_oracle(name, dim, n, ne, quad, monkeypatch):
+def test_integrate_sample_noise_vs_oracle(name, dim, n, ne, quad, knobs):
     """Positive shifts: the default picks the per-column factorisations at these ne (fewer
     columns than one eigendecomposition costs); GPR_QUAD_EIGEN=1 forces the eigensolver."""
     if quad != "auto":
-        monkeypatch.setenv("GPR_QUAD_EIGEN", quad)
+        knobs("GPR_QUAD_EIGEN", int(quad))
     kinds = [O.SE] if name == "SE" else [O.SE, O.WN]
     cov = G.SquaredExp() if name == "SE" else G.SquaredExp() + G.WhiteNoise()
     rng = np.random.default_rng(dim + n)
@@ -145,7 +145,7 @@ def test_integrate_sample_noise_vs_oracle(name, dim, n, ne, quad, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_integrate_sample_noise_negative(monkeypatch):
+def test_integrate_sample_noise_negative(knobs):
     """Negative sample noise, as the reference's eigen path takes it (src/integrate.jl:71-100:
     K = P Lambda P' once, (Lambda + noise_j)^-1 per column, never a factorisation): a shift
     that keeps K + noise I positive definite and one that makes it negative definite both
@@ -170,7 +170,7 @@ def test_integrate_sample_noise_negative(monkeypatch):
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, neg)
     np.testing.assert_allclose(I, Io, rtol=1e-8)
     np.testing.assert_allclose(v, vo, rtol=1e-8)
-    monkeypatch.setenv("GPR_QUAD_EIGEN", "0")
+    knobs("GPR_QUAD_EIGEN", 0)
     with pytest.raises(G.PosDefException):
         G.integrate(md, a, b, sample_noise=neg)
 
@@ -219,7 +219,7 @@ def test_integrate_inverse_perturbation_reference(dim, n, ne):
 
 
 @pytest.mark.gpu
-def test_integrate_auto_falls_back_to_eigen_when_not_posdef(monkeypatch):
+def test_integrate_auto_falls_back_to_eigen_when_not_posdef(knobs):
     """Nonnegative shifts on a singular K (every point the same, no jitter: K = sigma^2 1 1^T,
     the second pivot exactly 0): the default's per-column factorisation fails and hands the
     call to the eigensolver -- no PosDefException, the eigensolver's own result bit for bit."""
@@ -232,18 +232,18 @@ def test_integrate_auto_falls_back_to_eigen_when_not_posdef(monkeypatch):
     a, b = np.zeros(dim), np.ones(dim)
     noise = np.zeros(ne)
     I, v = G.integrate(md, a, b, sample_noise=noise, eps=0.0)
-    monkeypatch.setenv("GPR_QUAD_EIGEN", "1")
+    knobs("GPR_QUAD_EIGEN", 1)
     I1, v1 = G.integrate(md, a, b, sample_noise=noise, eps=0.0)
     np.testing.assert_array_equal(I, I1)
     np.testing.assert_array_equal(v, v1)
-    monkeypatch.setenv("GPR_QUAD_EIGEN", "0")
+    knobs("GPR_QUAD_EIGEN", 0)
     with pytest.raises(G.PosDefException):
         G.integrate(md, a, b, sample_noise=noise, eps=0.0)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,ne", [(300, 9), (1040, 6)])
-def test_integrate_batched_columns_chunking_and_sequential(n, ne, monkeypatch):
+def test_integrate_batched_columns_chunking_and_sequential(n, ne, knobs):
     """The default's batched launch (every K + s_j I factored and solved in one tile-DAG
     launch) is the same computation per column whatever the batch: a 1-column memory budget
     (GPR_QUAD_BATCH_GB, one launch per column) gives bit for bit the same result; the
@@ -258,12 +258,12 @@ def test_integrate_batched_columns_chunking_and_sequential(n, ne, monkeypatch):
     a, b = np.zeros(dim), np.ones(dim)
     noise = 1e-3 * (1.0 + rng.random(ne))
     I, v = G.integrate(md, a, b, sample_noise=noise)
-    monkeypatch.setenv("GPR_QUAD_BATCH_GB", "1e-9")
+    knobs("GPR_QUAD_BATCH_GB", 1e-9)
     I1, v1 = G.integrate(md, a, b, sample_noise=noise)
     np.testing.assert_array_equal(I, I1)
     np.testing.assert_array_equal(v, v1)
-    monkeypatch.delenv("GPR_QUAD_BATCH_GB")
-    monkeypatch.setenv("GPR_QUAD_SEQ", "1")
+    knobs("GPR_QUAD_BATCH_GB", 16.0)
+    knobs("GPR_QUAD_SEQ", 1)
     Is, vs = G.integrate(md, a, b, sample_noise=noise)
     np.testing.assert_allclose(Is, I, rtol=1e-9)
     np.testing.assert_allclose(vs, v, rtol=1e-8, atol=1e-12 * O.antideriv2_se(hp, a, b))

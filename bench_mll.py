@@ -50,7 +50,7 @@ def cpu_baseline(a, hp):
     """The CPU oracle (test infrastructure; this leg only) on a bounded sample of the C4
     evaluation: loss_grad! for an MllGradCache in the reference's order (src/cost.jl:83-126 --
     K, cholesky!, ldiv!, K^{-1} = ldiv!(kchol, I), the MLL and every dK/dtheta_i's
-    grad(MLL, ...) term, LogScale) at N = a.cpu_n, d = a.d, median of 3 after a warm-up, each
+    grad(MLL, ...) term, LogScale) at N = a.cpu_n, d = a.d, one run after a warm-up, each
     stage scaled to N = a.n by its complexity (N^2, N^3, N^2, N^3, N^2).  Threads: the box's CPU
     share (OMP_NUM_THREADS) for OpenBLAS, reported by threadpoolctl."""
     import scipy.linalg as sla
@@ -87,9 +87,8 @@ def cpu_baseline(a, hp):
                  "threads": i.get("num_threads")}
                 for i in threadpool_info() if i.get("user_api") == "blas"
                 and "scipy.libs" in i.get("filepath", "")]
-        run()
-        reps = [run() for _ in range(3)]
-    t = np.median(np.stack(reps), axis=0)
+        run()  # (warm-up)
+        t = run()  # one timed run: its 18 dK/dtheta terms alone take ~20 s at N = 4096
     r = a.n / n
     scale = np.array([r ** 2, r ** 3, r ** 2, r ** 3, r ** 2])
     t_eval = float(np.sum(t * scale))
@@ -98,7 +97,7 @@ def cpu_baseline(a, hp):
         "kind": "port", "blas": blas,
         "measured_config": {"N": n, "d": d, "stage_s": [round(v, 4) for v in t.tolist()]},
         "sample": (f"oracle (NumPy/SciPy OpenBLAS, {threads} threads) C4 evaluation at N={n}, "
-                   f"d={d} (median of 3 after 1 warm-up): stages [kernel, dpotrf, dpotrs, "
+                   f"d={d} (one run after 1 warm-up): stages [kernel, dpotrf, dpotrs, "
                    f"K^-1, mll+{len(hp)} grad terms] = {[round(v, 4) for v in t.tolist()]} s; "
                    f"extrapolated to N={a.n} by N^2 / N^3 / N^2 / N^3 / N^2 -> {t_eval:.2f} s "
                    f"per evaluation"),

@@ -55,7 +55,8 @@ def cpu_baseline(a, hp, xe, xq):
     predict(md, Cmap(+, xe, xq); diagonal_var=true) in the reference's order (src/predict.jl:
     29-34 fit, src/split_predict.jl:5-53 split factors, mean, variance rows) at ns = a.cpu_ns on
     the same 1024 x 1024 grid and variance rows, median of 3 after a warm-up; stages scaled to
-    ns = a.ns by their complexity (fit ns^3, split factors + mean ns, variance rows ns^2).
+    ns = a.ns by their complexity (K ns^2, dpotrf ns^3, split factors + mean ns, variance
+    rows ns^2).
     Threads: OMP_NUM_THREADS for OpenBLAS, reported by threadpoolctl."""
     from threadpoolctl import threadpool_info, threadpool_limits
 
@@ -71,7 +72,9 @@ def cpu_baseline(a, hp, xe, xq):
 
     def run():
         t0 = time.perf_counter()
-        U = O.chol_upper(O.kernel(kinds, hp, x))
+        K = O.kernel(kinds, hp, x)
+        tk = time.perf_counter()
+        U = O.chol_upper(K)
         wt = O.cho_solve_upper(U, y)
         t1 = time.perf_counter()
         mu, _ = O.split_predict_from_factor(kinds, hp, x, U, wt, xe, xq, var_range=None)
@@ -80,7 +83,7 @@ def cpu_baseline(a, hp, xe, xq):
                                              mean_rows=[0])
         t3 = time.perf_counter()
         assert np.isfinite(mu).all() and np.isfinite(var).all()
-        return np.array([t1 - t0, t2 - t1, t3 - t2])
+        return np.array([tk - t0, t1 - tk, t2 - t1, t3 - t2])
 
     with threadpool_limits(limits=threads):
         blas = [{"lib": i.get("internal_api"), "version": i.get("version"),
@@ -91,7 +94,7 @@ def cpu_baseline(a, hp, xe, xq):
         reps = [run() for _ in range(3)]
     t = np.median(np.stack(reps), axis=0)
     r = a.ns / ns
-    scale = np.array([r ** 3, r, r ** 2])
+    scale = np.array([r ** 2, r ** 3, r, r ** 2])
     t_job = float(np.sum(t * scale))
     return {
         "value": a.ne * a.nq / t_job, "unit": "test points/s", "cores": threads, "kind": "port",
@@ -100,9 +103,9 @@ def cpu_baseline(a, hp, xe, xq):
                             "stage_s": [round(v, 4) for v in t.tolist()]},
         "sample": (f"oracle (NumPy/SciPy OpenBLAS, {threads} threads) C5 job at ns={ns}, "
                    f"{a.ne}x{a.nq} grid, {a.var_rows} variance rows (median of 3 after 1 "
-                   f"warm-up): stages [fit, split factors + mean, variance rows] = "
-                   f"{[round(v, 4) for v in t.tolist()]} s; extrapolated to ns={a.ns} by ns^3 / "
-                   f"ns / ns^2 -> {t_job:.2f} s per job"),
+                   f"warm-up): stages [kernel, dpotrf + dpotrs, split factors + mean, variance rows] = "
+                   f"{[round(v, 4) for v in t.tolist()]} s; extrapolated to ns={a.ns} by ns^2 / "
+                   f"ns^3 / ns / ns^2 -> {t_job:.2f} s per job"),
     }
 
 

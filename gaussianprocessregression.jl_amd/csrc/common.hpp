@@ -171,8 +171,12 @@ struct gpr_ctx {
   int kup_n = 0, kup_ld = 0;
   double* dagb = nullptr;       // batched tile-DAG workspace (W slots, task lists, counters)
   size_t dagb_cap = 0;
-  double* deig = nullptr;       // block-Jacobi eigensolver workspace (eigen.hip)
+  double* deig = nullptr;       // eigensolver workspace (eigen.hip, tridiag.hip)
   size_t eig_cap = 0;
+  double* ddc = nullptr;        // divide-and-conquer workspace (dstedc.hip)
+  size_t dc_cap = 0;
+  double* dtri = nullptr;       // the tridiagonal T between the two stages
+  size_t tri_cap = 0;
   int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)
   int kbuild_exact = 0;         // GPR_KBUILD_EXACT=1: the reference's difference form for K
   int cv_batch = 1;             // GPR_CV_BATCH=0: cv_batch folds one by one on child contexts
@@ -308,11 +312,25 @@ int trsm_ut_core(gpr_ctx* ctx, const double* dU, int n, int ldu, double* dB, int
                  int ldb, double* norm_out, int lower_rhs);
 int kinv_from_z(gpr_ctx* ctx, const double* Z, int n, double* dKinv, int ldk);
 // symmetric eigendecomposition A = P diag(lam) P^T applied to B: lam (n, device) and
-// B <- P^T B (n x m, ld ldb), A read only (eigen.hip, block Jacobi); *sweeps may be null.
-// floor >= 0: the eigenvalues of A + floor I to high relative accuracy (what (lam + s)^-1 needs
-// for every s >= floor); 0 = those of A itself
+// B <- P^T B (n x m, ld ldb), A read only; *sweeps may be null.  method 0: tridiagonal
+// reduction + divide and conquer (tridiag.hip, dstedc.hip) where n fits them, else block
+// Jacobi (eigen.hip); 2: block Jacobi, whose floor >= 0 asks for the eigenvalues of A + floor I
+// to high relative accuracy (what (lam + s)^-1 needs for every s >= floor; 0 = those of A)
 int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
-                  double* dlam, int* sweeps, double floor = 0.0);
+                  double* dlam, int* sweeps, double floor, int method);
+// dstedc.hip: T = tridiag(e, d, e) = Z diag(lam) Z^T, C <- Z^T C; n <= 6144 (tridiag_eig_ok)
+int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, double* dC, int m,
+                      int ldc, double* dlam);
+bool tridiag_eig_ok(int n);
+// tridiag.hip: A = Q T Q^T (d, e on the device; B <- Q^T B when m > 0), one persistent launch
+// + blocked WY back-transform; n <= 4608 (sym_tridiag_ok).  Workspace ctx->deig.
+int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                double* dd, double* de);
+bool sym_tridiag_ok(int n);
+// the quadrature's columns from T: out[2j] = C[:, j]' (T + s_j I)^{-1} c, out[2j+1] = k2 - c' (T +
+// s_j I)^{-1} c with c = C[:, ny]; scr: 4 n ny doubles
+int quad_tridiag_solves(gpr_ctx* ctx, const double* dd, const double* de, int n, const double* C,
+                        int ldc, int ny, const double* dnoise, double k2, double* scr, double* out);
 // norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream
 int launch_colnorm_sub(gpr_ctx* ctx, const double* dB, int ldb, int n, int ncols, double* norm);
 // forward = false: only the backward sweep U x = B (B already holds U^{-T} b);

@@ -484,8 +484,8 @@ __global__ void eig_diag_kernel(const double* __restrict__ W, int n2, int n, dou
 // B (n x m, ld ldb) <- P^T B with A = P diag(lambda) P^T.  Eigenvalues in no particular order,
 // B's rows in the same order.  *sweeps: outer sweeps used.  Returns GPR_E_HIP (with a message)
 // if the iteration does not converge within GPR_EIG_MAX_SWEEPS (default 60).
-int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
-                  double* dlam, int* sweeps_out, double floor) {
+static int jacobi_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m,
+                            int ldb, double* dlam, int* sweeps_out, double floor) {
   if (n <= 0) return 0;
   const int n2 = (n + ES - 1) / ES * ES;
   const int nb = n2 / EB, np = nb / 2;
@@ -532,11 +532,38 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
   return 0;
 }
 
+// The symmetric eigendecomposition applied to B: by default the tridiagonal reduction
+// (tridiag.hip: A = Q T Q^T, B <- Q^T B inside its launch) followed by divide and conquer on T
+// (dstedc.hip: lam, B <- Z^T B) -- LAPACK syevr's two stages; block Jacobi (above) for n beyond
+// their LDS bounds or when asked for (method 2).  *sweeps: Jacobi sweeps, or the depth of the
+// divide-and-conquer tree.
+int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                  double* dlam, int* sweeps_out, double floor, int method) {
+  if (n <= 0) {
+    if (sweeps_out) *sweeps_out = 0;
+    return 0;
+  }
+  if (method != 2 && sym_tridiag_ok(n) && tridiag_eig_ok(n)) {
+    GPR_TRY(ensure_buf(ctx, &ctx->dtri, &ctx->tri_cap, 2 * (size_t)n + 2));
+    double* d = ctx->dtri;
+    double* e = d + n + 1;
+    GPR_TRY(sym_tridiag(ctx, dA, n, lda, dB, m, ldb, d, e));
+    GPR_TRY(tridiag_eig_apply(ctx, d, e, n, dB, m, ldb, dlam));
+    if (sweeps_out) {
+      int depth = 0;
+      while ((1 << depth) < n) ++depth;
+      *sweeps_out = depth;
+    }
+    return 0;
+  }
+  return jacobi_eig_apply(ctx, dA, n, lda, dB, m, ldb, dlam, sweeps_out, floor);
+}
+
 extern "C" int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m,
                               int ldb, double* dlam, int* sweeps) {
   if (!ctx) return GPR_E_ARG;
   if (n < 0 || m < 0 || lda < std::max(n, 1) || (m > 0 && ldb < std::max(n, 1)) ||
       (n > 0 && (!dA || !dlam)) || (m > 0 && n > 0 && !dB))
     return set_err(ctx, GPR_E_ARG, "bad args");
-  return sym_eig_apply(ctx, dA, n, lda, dB, m, ldb, dlam, sweeps);
+  return sym_eig_apply(ctx, dA, n, lda, dB, m, ldb, dlam, sweeps, 0.0, 0);
 }

@@ -280,6 +280,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
   for (auto& e : ctx->kup)
     if (e.d) hipFree(e.d);
   if (ctx->deig) hipFree(ctx->deig);
+  if (ctx->ddc) hipFree(ctx->ddc);
+  if (ctx->dtri) hipFree(ctx->dtri);
   if (ctx->dagb) hipFree(ctx->dagb);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -1067,10 +1067,45 @@ __global__ __launch_bounds__(256) void quad_diag_update_kernel(const double* __r
 // (nothing done) when rocSOLVER cannot be loaded.
 static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k2, int n,
                              const double* dy, int ny, int ldy, const double* noise, double* Iout,
-                             double* var, bool rocsolver) {
+                             double* var, int method) {
+  const bool rocsolver = method == 2;
+  if (method == 1 && sym_tridiag_ok(n)) {
+    // K = Q T Q^T by the hand-written tridiagonal reduction (tridiag.hip; syevr's first
+    // stage), C = Q^T [Y | k1], then per column one tridiagonal solve with (T + noise_j I):
+    // Iout_j = C[:, j]' (T + s_j I)^{-1} C[:, ny] = k1' (K + s_j I)^{-1} y_j -- the reference's
+    // sum_i (P'y_j)_i (P'k1)_i / (lambda_i + s_j) without the eigenvectors (any shift)
+    const size_t nc = (size_t)n * (ny + 1);
+    GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap,
+                       nc + 2 * (size_t)n + 3 * (size_t)ny + 4 * (size_t)n * ny));
+    double* C = ctx->dbig;
+    double* dd = C + nc;
+    double* de = dd + n;
+    double* dnoise = de + n;
+    double* out = dnoise + ny;
+    double* scr = out + 2 * (size_t)ny;
+    HIP_TRY(ctx, hipMemcpy2DAsync(C, sizeof(double) * n, dy, sizeof(double) * ldy,
+                                  sizeof(double) * n, ny, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(C + (size_t)ny * n, k1, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise, sizeof(double) * ny, hipMemcpyHostToDevice,
+                                ctx->stream));
+    GPR_TRY(sym_tridiag(ctx, K, n, n, C, ny + 1, n, dd, de));
+    GPR_TRY(quad_tridiag_solves(ctx, dd, de, n, C, n, ny, dnoise, k2, scr, out));
+    std::vector<double> h(2 * (size_t)ny);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), out, sizeof(double) * 2 * ny, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int j = 0; j < ny; ++j) {
+      Iout[j] = h[2 * j];
+      var[j] = h[2 * j + 1];
+    }
+    return 0;
+  }
   if (!rocsolver) {
-    // the hand-written block-Jacobi eigensolver (eigen.hip): lambda and T = P^T [Y | k1]
-    // directly, P never formed
+    // the full eigendecomposition, as the reference (method 3; method 1 beyond the reduction's
+    // LDS bound): K = P Lambda P^T by the tridiagonal reduction + divide and conquer, or by block
+    // Jacobi (method 4, or n beyond both), lambda and T = P^T [Y | k1] directly, P never formed;
+    // then the reference's diagonal update per column
     const size_t nb = (size_t)n * (ny + 1);
     GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap, nb + (size_t)n + 3 * (size_t)ny));
     double* T = ctx->dbig;
@@ -1086,7 +1121,8 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
     // relative accuracy for K + s_min I (s_min = the smallest shift when none is negative)
     double smin = noise[0];
     for (int j = 1; j < ny; ++j) smin = std::min(smin, noise[j]);
-    GPR_TRY(sym_eig_apply(ctx, K, n, n, T, ny + 1, n, lam, nullptr, std::max(smin, 0.0)));
+    GPR_TRY(sym_eig_apply(ctx, K, n, n, T, ny + 1, n, lam, nullptr, std::max(smin, 0.0),
+                          method == 4 ? 2 : 0));
     quad_diag_update_kernel<<<ny, 256, 0, ctx->stream>>>(T, n, ny, lam, dnoise, k2, out);
     LAUNCH_CHECK(ctx);
     std::vector<double> h(2 * (size_t)ny);
@@ -1196,7 +1232,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
     fallback = qmode == 0;
   }
   if (qmode != 0) {
-    const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode == 2);
+    const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode);
     if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
   }
   if (!ctx->quad_seq) {  // the batched launch (GPR_QUAD_SEQ: one column at a time)
@@ -1206,7 +1242,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
     if (!declined) {
       if (rc > 0 && fallback) {  // K + s I not numerically positive definite: the eigensolver
         ctx->err.clear();
-        return integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, false);
+        return integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, 1);
       }
       return rc;
     }
@@ -1226,7 +1262,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   }
   if (rc > 0 && fallback) {  // K + s I not numerically positive definite: the eigensolver
     ctx->err.clear();
-    return integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, false);
+    return integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, 1);
   }
   return rc;
 }

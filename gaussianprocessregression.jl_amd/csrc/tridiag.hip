@@ -1,0 +1,621 @@
+// Symmetric tridiagonal reduction, hand-written for gfx950: the first stage of LAPACK's syevr
+// (dsytrd) behind the sample_noise quadrature (src/integrate.jl:71-100, LAPACK.syevr! at :75).
+//
+//   A = Q T Q^T,  T = tridiag(e, d, e),  Q = H_0 H_1 ... H_{n-3},  H_j = I - tau_j v_j v_j^T
+//
+// (v_j lives on rows j+1..n-1 with v_j[j+1] = 1; dlarfg's reflector conventions).  The
+// quadrature never needs an eigenvector: k1' (K + s I)^{-1} y = (Q^T k1)' (T + s I)^{-1} (Q^T y),
+// so after the reduction every column costs one O(n) tridiagonal solve (any shift: Gaussian
+// elimination with partial pivoting, dgtsv), and gpr_syev_apply's eigendecomposition
+// continues from T with the divide-and-conquer solver (dstedc.hip).
+//
+// The reduction: ONE persistent launch of P workgroups (~16 columns each, at most one per CU),
+// the unblocked two-sided Householder algorithm (dsytd2) on a full symmetric work copy,
+// columns dealt round-robin (column c to workgroup c mod P: contiguous, coalesced).  Step j,
+// with v_j, tau_j and (j > 0) v_{j-1}, w_{j-1} in every workgroup's LDS:
+//   * the pass: every workgroup, over its columns c > j, applies step j-1's rank-2 update
+//     A(:, c) -= v_{j-1} w_{j-1}[c] + w_{j-1} v_{j-1}[c] and forms p_j[c] = tau_j A(:, c) . v_j
+//     (each column read once and written once, 16-B accesses, 8 row pairs in flight per lane);
+//     the owner of column j + 1 also publishes that column;
+//   * one exchange: each workgroup publishes p_j[c] and its part of p_j . v_j and arrives on the
+//     step's counter; once all P have arrived every workgroup reads p_j, the partial sums and
+//     column j + 1 and forms w_j = p_j - (tau_j / 2)(p_j . v_j) v_j, column j + 1 after step j
+//     and the next reflector (dlarfg) ITSELF -- the same bits everywhere, so no second hop.
+// Hand-offs follow the MI355X guide's sc1 protocol (write-through stores drained before the
+// counter's atomic add, an sc1 poll, a workgroup barrier, sc1 loads), every handed-off address
+// written once per launch (p_j, column j + 1, the partial sums each have their own slot).  Every
+// wait is bounded (~4 s): on a time-out the launch drains and the call reports an error.
+//
+// Cost per step: one fan-in of P arrivals plus 2 (n - j) + P sc1 loads per workgroup, and the
+// pass (16 (n - j)^2 / P bytes per workgroup; the work copy stays in the Infinity Cache up to n
+// ~ 4k).
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int TRD_THREADS = 512;   // 8 waves: one column per wave at a time
+constexpr int TRD_WAVES = TRD_THREADS / 64;
+constexpr int TRD_MAXN = 6144;     // 3 LDS vectors of n doubles per workgroup
+constexpr int TRD_FUSED_M = 1024;  // right-hand sides transformed inside the launch
+
+__device__ __forceinline__ double ld1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld1i(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st1i(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+#ifdef GPR_TESTING
+// phase stamps of workgroups 0 and P-1 (test build only: tools/trd_trace.py)
+__device__ long long g_trd_trace[2][TRD_MAXN][6];
+#define TRD_STAMP(k)                                                                   \
+  do {                                                                                 \
+    if (tid == 0 && (w == 0 || w == P - 1))                                            \
+      g_trd_trace[w == 0 ? 0 : 1][j][k] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define TRD_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
+struct TrdArgs {
+  double* A;        // n x n work copy (full symmetric), ld lda; columns updated in place
+  size_t lda;
+  int n, P, ldl;    // ldl: stride of the LDS vectors (n rounded up to 2)
+  double* V;        // n x n (ld lda): column j = v_j on rows j+1..n-1 (v_j[j+1] = 1)
+  double* cpub;     // n x n (ld lda): column j + 1 after step j - 1, published by its owner
+  double* pbuf;     // n x n (ld lda): column j = p_j
+  double* parts;    // n x P partial sums p_j . v_j
+  double* tau;      // n (tau[n-2], tau[n-1] = 0)
+  double* d;        // n: diagonal of T
+  double* e;        // n - 1: off-diagonal of T
+  double* dlast;    // A(n-1, n-1) after step n - 4's update (from the owner of column n-1)
+  int* cnt;         // n: arrivals of step j's pass
+  int* err;         // set on a wait time-out: every wait then gives up
+  long long spin_limit;
+  double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
+  size_t ldb;
+  int m;
+};
+
+// lane 0 polls *p >= v (sc1), giving up on a time-out or another workgroup's error; the whole
+// workgroup leaves together.  Returns false on error.
+__device__ bool trd_wait(const TrdArgs& a, const int* p, int v, int* s_ok) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    long long spins = 0;
+    while (ld1i(p) < v) {
+      if (ld1i(a.err)) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > a.spin_limit) {
+        st1i(a.err, 1);
+        ok = 0;
+        break;
+      }
+    }
+    *s_ok = ok;
+  }
+  __syncthreads();
+  const bool ok = *s_ok != 0;
+  __syncthreads();
+  return ok;
+}
+
+// workgroup sum of one value per thread (red: >= TRD_WAVES doubles of LDS), deterministic: the
+// same inputs give the same bits in every workgroup
+__device__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int q = 0; q < TRD_WAVES; ++q) s += red[q];
+  __syncthreads();
+  return s;
+}
+
+// dlarfg on col[j+1..n-1] in place -> v_j (v_j[j+1] = 1); returns tau_j, *beta = e_j.  Every
+// workgroup computes the same bits (the reflector is formed redundantly everywhere).
+__device__ double trd_reflector(int n, int j, double* col, double* red, double* beta_out) {
+  double s = 0.0;
+  for (int r = j + 2 + threadIdx.x; r < n; r += TRD_THREADS) s += col[r] * col[r];
+  const double xnorm2 = block_sum(s, red);
+  const double alpha = col[j + 1];
+  double tau = 0.0, beta = alpha, scal = 0.0;
+  if (xnorm2 > 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+  }
+  for (int r = j + 1 + threadIdx.x; r < n; r += TRD_THREADS) col[r] = r == j + 1 ? 1.0 : col[r] * scal;
+  __syncthreads();
+  *beta_out = beta;
+  return tau;
+}
+
+// Step j's state, identical in every workgroup: vcur = v_j, tau_j; (j > 0) vprev = v_{j-1},
+// wprev = w_{j-1}.  One exchange per step: the pass publishes p_j (and the owner of column
+// j + 1 that column), every workgroup then forms w_j, column j + 1 and v_{j+1} itself.
+__global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
+  extern __shared__ double lds[];
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int n = a.n, P = a.P, w = blockIdx.x, L = a.ldl;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double* red = lds + 3 * (size_t)L;
+  int* s_ok = reinterpret_cast<int*>(red + TRD_WAVES);
+  int ivp = 0, iwp = 1, ivc = 2;
+  double tj;
+
+  {  // v_0 from column 0 (no update before it), redundantly in every workgroup
+    double* c = lds + (size_t)ivc * L;
+    for (int r = tid; r < n; r += TRD_THREADS) c[r] = a.A[r];
+    __syncthreads();
+    const double d0 = c[0];
+    double beta;
+    tj = trd_reflector(n, 0, c, red, &beta);
+    if (w == 0 && tid == 0) {
+      a.d[0] = d0;
+      a.e[0] = beta;
+      a.tau[0] = tj;
+    }
+    if (w == 0)
+      for (int r = 1 + tid; r < n; r += TRD_THREADS) a.V[r] = c[r];
+  }
+
+  for (int j = 0; j <= n - 3; ++j) {
+    const double* vprev = lds + (size_t)ivp * L;
+    const double* wprev = lds + (size_t)iwp * L;
+    const double* vcur = lds + (size_t)ivc * L;
+    // ---- the pass over this workgroup's columns c > j, one wave per column: rows from the
+    // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), 8 row pairs
+    // in flight per lane
+    TRD_STAMP(0);
+    double sp = 0.0;
+    const int r0 = (j + 1) & ~1;
+    const int c0 = w + ((j + 1 - w + P - 1) / P) * P;  // first owned column > j
+    for (int c = c0 + wv * P; c < n; c += TRD_WAVES * P) {
+      double* col = a.A + (size_t)c * a.lda;
+      const double wc = j > 0 ? wprev[c] : 0.0, vc = j > 0 ? vprev[c] : 0.0;
+      double* pub = c == j + 1 ? a.cpub + (size_t)(j + 1) * a.lda : nullptr;
+      double dot = 0.0;
+      for (int rb = r0 + 2 * lane; rb < n; rb += 16 * 64) {
+        d2 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = rb + 128 * u;
+          if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = rb + 128 * u;
+          if (r < n) {
+            const d2 vp = *reinterpret_cast<const d2*>(vprev + r);
+            const d2 wp = *reinterpret_cast<const d2*>(wprev + r);
+            const d2 vv = *reinterpret_cast<const d2*>(vcur + r);
+            if (j > 0) {
+              x[u].x -= vp.x * wc + wp.x * vc;
+              x[u].y -= vp.y * wc + wp.y * vc;
+              *reinterpret_cast<d2*>(col + r) = x[u];
+            }
+            if (pub) {
+              st1(pub + r, x[u].x);
+              st1(pub + r + 1, x[u].y);
+            }
+            if (c == n - 1 && j == n - 3) {  // A(n-1, n-1) for the last 2 x 2 block
+              if (r == n - 1) st1(a.dlast, x[u].x);
+              if (r + 1 == n - 1) st1(a.dlast, x[u].y);
+            }
+            // (row j and, for odd n, the padding row n are outside v_j's support)
+            dot += (r >= j + 1 ? x[u].x * vv.x : 0.0) + (r + 1 < n ? x[u].y * vv.y : 0.0);
+          }
+        }
+      }
+      const double p = tj * wave_sum(dot);
+      if (lane == 0) st1(&a.pbuf[(size_t)j * a.lda + c], p);
+      sp += p * vcur[c];
+    }
+    // ---- Q^T B on the fly: H_j applied to this workgroup's columns of B (v_j is in every
+    // workgroup's LDS, so no exchange): b -= tau_j (v_j . b) v_j, rows j+1..n-1
+    for (int c = w + wv * P; c < a.m; c += TRD_WAVES * P) {
+      double* b = a.B + (size_t)c * a.ldb;
+      double dot = 0.0;
+      for (int rb = j + 1 + lane; rb < n; rb += 4 * 64) {
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = rb + 64 * u < n ? b[rb + 64 * u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (rb + 64 * u < n) dot += x[u] * vcur[rb + 64 * u];
+      }
+      const double f = tj * wave_sum(dot);
+      for (int r = j + 1 + lane; r < n; r += 64) b[r] -= f * vcur[r];
+    }
+    // ---- publish this workgroup's part of p_j . v_j, arrive, wait for every workgroup
+    TRD_STAMP(1);
+    if (lane == 0) red[wv] = sp;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < TRD_WAVES; ++q) s += red[q];
+      st1(&a.parts[(size_t)j * P + w], s);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&a.cnt[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    TRD_STAMP(2);
+    if (!trd_wait(a, &a.cnt[j], P, s_ok)) return;
+    TRD_STAMP(3);
+    // ---- w_j, column j + 1 after step j, v_{j+1}: the same bits in every workgroup.  Every
+    // load of the exchange is issued at once (partial sums, p_j, the published column); the
+    // column update also sums the reflector's x-norm.
+    double* wnew = lds + (size_t)ivp * L;  // (v_{j-1}'s slot)
+    double* cnew = lds + (size_t)iwp * L;  // (w_{j-1}'s slot) -> v_{j+1}
+    const double* pj = a.pbuf + (size_t)j * a.lda;
+    const double* cp = a.cpub + (size_t)(j + 1) * a.lda;
+    constexpr int RPT = (TRD_MAXN + TRD_THREADS - 1) / TRD_THREADS;
+    double pr[RPT], cr[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = j + 1 + tid + k * TRD_THREADS;
+      pr[k] = r < n ? ld1(&pj[r]) : 0.0;
+      cr[k] = r < n ? ld1(&cp[r]) : 0.0;
+    }
+    const double pc = ld1(&pj[j + 1]);
+    double s = 0.0;
+    for (int q = tid; q < P; q += TRD_THREADS) s += ld1(&a.parts[(size_t)j * P + q]);
+    const double kj = 0.5 * tj * block_sum(s, red);
+    TRD_STAMP(4);
+    const double wc = pc - kj * vcur[j + 1], vc = vcur[j + 1];
+    double xn = 0.0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = j + 1 + tid + k * TRD_THREADS;
+      if (r < n) {
+        const double wr = pr[k] - kj * vcur[r];
+        const double x = cr[k] - (vcur[r] * wc + wr * vc);
+        wnew[r] = wr;
+        cnew[r] = x;
+        if (r >= j + 3) xn += x * x;
+      }
+    }
+    const double xnorm2 = block_sum(xn, red);  // (its barriers publish cnew / wnew)
+    const bool out = w == (j + 1) % P;         // (one workgroup writes T and V)
+    if (out && tid == 0) a.d[j + 1] = cnew[j + 1];
+    if (j + 1 <= n - 3) {
+      // dlarfg on cnew[j+2..n-1] -> v_{j+1} in place
+      const double alpha = cnew[j + 2];
+      double tau = 0.0, beta = alpha, scal = 0.0;
+      if (xnorm2 > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
+        tau = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+      }
+      double* vj = a.V + (size_t)(j + 1) * a.lda;
+      for (int r = j + 2 + tid; r < n; r += TRD_THREADS) {
+        const double v = r == j + 2 ? 1.0 : cnew[r] * scal;
+        cnew[r] = v;
+        if (out) vj[r] = v;
+      }
+      if (out && tid == 0) {
+        a.e[j + 1] = beta;
+        a.tau[j + 1] = tau;
+      }
+      tj = tau;
+      __syncthreads();
+    } else if (out && tid == 0) {  // the last 2 x 2 block: e_{n-2}, d_{n-1}
+      a.e[n - 2] = cnew[n - 1];
+      a.d[n - 1] = ld1(a.dlast) - 2.0 * vcur[n - 1] * wnew[n - 1];
+    }
+    TRD_STAMP(5);
+    const int t = ivp;
+    ivp = ivc;
+    ivc = iwp;
+    iwp = t;
+  }
+}
+
+// ---- Q^T B by blocks of reflectors (compact WY, dlarft forward / columnwise) --------------
+constexpr int QB = 64;  // reflectors per block
+
+// Vb (n2 x QB, ld n2) and VbT (QB x n2, ld QB): column i = v_{j0+i} (zeros above row j0+i+1,
+// zero columns past the last reflector)
+__global__ void qblock_prep_kernel(const double* __restrict__ V, size_t ldv, int n, int n2,
+                                   int j0, int nref, double* __restrict__ Vb,
+                                   double* __restrict__ VbT) {
+  const size_t tot = (size_t)n2 * QB;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < tot;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t % n2), i = (int)(t / n2);
+    const int j = j0 + i;
+    const double v = (i < nref && r > j && r < n) ? V[(size_t)j * ldv + r] : 0.0;
+    Vb[t] = v;
+    VbT[(size_t)i + (size_t)r * QB] = v;
+  }
+}
+
+// T (QB x QB upper, ld QB) from G = Vb^T Vb and tau: T(i,i) = tau_i, T(0:i, i) = -tau_i
+// T(0:i, 0:i) G(0:i, i) (dlarft forward / columnwise); unused columns (i >= nref) zero
+__global__ __launch_bounds__(QB) void qblock_t_kernel(const double* __restrict__ G,
+                                                     const double* __restrict__ tau, int j0,
+                                                     int nref, double* __restrict__ T) {
+  __shared__ double Ts[QB][QB + 1];
+  __shared__ double g[QB];
+  const int k = threadIdx.x;
+  for (int i = 0; i < QB; ++i) Ts[k][i] = 0.0;
+  __syncthreads();
+  for (int i = 0; i < nref; ++i) {
+    const double ti = tau[j0 + i];
+    g[k] = k < i ? -ti * G[k + (size_t)i * QB] : 0.0;
+    __syncthreads();
+    double s = 0.0;
+    if (k < i)
+      for (int l = k; l < i; ++l) s += Ts[k][l] * g[l];
+    __syncthreads();
+    if (k < i) Ts[k][i] = s;
+    if (k == i) Ts[i][i] = ti;
+    __syncthreads();
+  }
+  for (int i = 0; i < QB; ++i) T[k + (size_t)i * QB] = Ts[k][i];
+}
+
+// ---- the quadrature's per-column solves on T ---------------------------------------------
+// Column j (one thread): x = (T + s_j I)^{-1} c with c = C[:, ny] = Q^T k1 by Gaussian
+// elimination with partial pivoting on the tridiagonal (dgtsv: the row interchanges fill a
+// second superdiagonal), then out[2j] = C[:, j] . x (= k1' (K + s_j I)^{-1} y_j, Iout) and
+// out[2j+1] = k2 - c . x (var).  Scratch: 4 n doubles per column.
+__global__ void quad_tridiag_kernel(const double* __restrict__ d, const double* __restrict__ e,
+                                    int n, const double* __restrict__ C, size_t ldc, int ny,
+                                    const double* __restrict__ noise, double k2,
+                                    double* __restrict__ scr, double* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ny) return;
+  const double s = noise[j];
+  const double* c = C + (size_t)ny * ldc;
+  double* Dm = scr + (size_t)j * 4 * n;  // final pivots
+  double* U1 = Dm + n;                   // first superdiagonal
+  double* U2 = U1 + n;                   // second superdiagonal (row interchanges)
+  double* x = U2 + n;                    // right-hand side -> solution
+  if (n == 1) {
+    const double x0 = c[0] / (d[0] + s);
+    out[2 * j] = C[(size_t)j * ldc] * x0;
+    out[2 * j + 1] = k2 - c[0] * x0;
+    return;
+  }
+  // running row i: (Di, Ui) on the diagonal / superdiagonal, bi; next row: (L = e_i, Dn, Un)
+  double Di = d[0] + s, Ui = e[0], bi = c[0];
+  for (int i = 0; i < n - 1; ++i) {
+    const double L = e[i];
+    const double Dn = d[i + 1] + s;
+    const double Un = i + 1 < n - 1 ? e[i + 1] : 0.0;
+    const double bn = c[i + 1];
+    if (fabs(Di) >= fabs(L)) {  // no interchange
+      const double f = L / Di;
+      Dm[i] = Di;
+      U1[i] = Ui;
+      U2[i] = 0.0;
+      x[i] = bi;
+      Di = Dn - f * Ui;
+      Ui = Un;
+      bi = bn - f * bi;
+    } else {  // rows i and i + 1 swap: row i becomes (L, Dn, Un), the next (Di, Ui, 0) - f row i
+      const double f = Di / L;
+      Dm[i] = L;
+      U1[i] = Dn;
+      U2[i] = Un;
+      x[i] = bn;
+      const double nd = Ui - f * Dn;
+      const double nu = -f * Un;
+      const double nb = bi - f * bn;
+      Di = nd;
+      Ui = nu;
+      bi = nb;
+    }
+  }
+  Dm[n - 1] = Di;
+  x[n - 1] = bi;
+  // back substitution, dotting as it goes
+  const double* cy = C + (size_t)j * ldc;
+  double x2 = 0.0, x1 = bi / Di;
+  double si = cy[n - 1] * x1, sv = c[n - 1] * x1;
+  for (int i = n - 2; i >= 0; --i) {
+    const double xi = (x[i] - U1[i] * x1 - U2[i] * x2) / Dm[i];
+    si += cy[i] * xi;
+    sv += c[i] * xi;
+    x2 = x1;
+    x1 = xi;
+  }
+  out[2 * j] = si;
+  out[2 * j + 1] = k2 - sv;
+}
+
+__global__ void trd_copy_kernel(const double* __restrict__ A, size_t lda, int n,
+                                double* __restrict__ W, size_t ldw) {
+  const size_t tot = (size_t)n * n;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < tot;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t % n), c = (int)(t / n);
+    W[(size_t)r + (size_t)c * ldw] = A[(size_t)r + (size_t)c * lda];
+  }
+}
+
+}  // namespace
+
+// A (n x n, lda; symmetric, both triangles read) = Q T Q^T: d[n], e[n-1] (device) and, when
+// m > 0, B <- Q^T B (n x m, ldb).  Workspace in ctx->deig.  n <= TRD_MAXN.
+int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                double* dd, double* de) {
+  if (n <= 0) return 0;
+  if (n > TRD_MAXN) return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: n = %d > %d", n, TRD_MAXN);
+  hipStream_t st = ctx->stream;
+  if (ctx->ncu <= 0) {
+    hipDeviceProp_t prop;
+    HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
+    ctx->ncu = prop.multiProcessorCount;
+  }
+  const size_t ld = (size_t)(n + 15) / 16 * 16;
+  // workgroups: ~16 columns each (two per wave), at most one per CU
+  const int P = std::max(1, std::min(ctx->ncu, (n + 15) / 16));
+  // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), tau, dlast, then ints
+  const size_t nW = ld * n;
+  const size_t nI = (size_t)n + 2;  // counters, err (as doubles: half of it, rounded up)
+  const int n2 = (int)ld;
+  // B <- Q^T B inside the launch (each workgroup applies H_j to its columns of B as v_j
+  // appears) up to TRD_FUSED_M columns; wider B (e.g. gpr_syev_apply on B = I) by blocks of
+  // 64 reflectors on the MFMA GEMM afterwards
+  const bool fused_b = m > 0 && m <= TRD_FUSED_M;
+  const size_t nQ = (m > 0 && !fused_b) ? 2 * (size_t)n2 * QB + 2 * (size_t)QB * QB + 2 * (size_t)QB * m : 0;
+  const size_t need = 4 * nW + (size_t)n * P + (size_t)n + 8 + nI + nQ;
+  GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
+  double* W = ctx->deig;
+  double* V = W + nW;
+  double* cpub = V + nW;
+  double* pbuf = cpub + nW;
+  double* parts = pbuf + nW;
+  double* tau = parts + (size_t)n * P;
+  double* dlast = tau + n;
+  int* ints = reinterpret_cast<int*>(dlast + 8);
+  int* cnt = ints;
+  int* err = ints + n;
+  double* Vb = reinterpret_cast<double*>(ints) + nI;  // the Q^T B blocks'
+  TimerScope ts(ctx, TC_OTHER, 4.0 * n * (double)n * n / 3.0);
+  if (n == 1 || n == 2) {  // already tridiagonal: T = A, Q = I
+    HIP_TRY(ctx, hipMemcpy2DAsync(dd, sizeof(double), dA, sizeof(double) * (lda + 1),
+                                  sizeof(double), n, hipMemcpyDeviceToDevice, st));
+    if (n == 2) HIP_TRY(ctx, hipMemcpyAsync(de, dA + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
+    return 0;
+  }
+  trd_copy_kernel<<<1024, 256, 0, st>>>(dA, (size_t)lda, n, W, ld);
+  LAUNCH_CHECK(ctx);
+  HIP_TRY(ctx, hipMemsetAsync(ints, 0, sizeof(int) * ((size_t)n + 2), st));
+  HIP_TRY(ctx, hipMemsetAsync(tau, 0, sizeof(double) * n, st));
+  TrdArgs a{};
+  a.A = W;
+  a.lda = ld;
+  a.n = n;
+  a.P = P;
+  a.ldl = (n + 1) & ~1;
+  a.V = V;
+  a.cpub = cpub;
+  a.pbuf = pbuf;
+  a.parts = parts;
+  a.tau = tau;
+  a.d = dd;
+  a.e = de;
+  a.dlast = dlast;
+  a.cnt = cnt;
+  a.err = err;
+  a.spin_limit = 1ll << 24;
+  a.B = fused_b ? dB : nullptr;
+  a.ldb = (size_t)ldb;
+  a.m = fused_b ? m : 0;
+  const size_t shmem = (3 * (size_t)a.ldl + TRD_WAVES) * sizeof(double) + 16;
+  sytrd_kernel<<<P, TRD_THREADS, shmem, st>>>(a);
+  LAUNCH_CHECK(ctx);
+  int herr = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(ctx, hipStreamSynchronize(st));
+  if (herr) return set_err(ctx, GPR_E_HIP, "tridiagonal reduction: a wait timed out");
+  if (m <= 0 || fused_b) return 0;
+  // B <- Q^T B = H_{n-3} ... H_0 B, 64 reflectors per block: B -= V_b (T_b^T (V_b^T B))
+  const int nref_all = n - 2;
+  double* VbT = Vb + (size_t)n2 * QB;
+  double* G = VbT + (size_t)n2 * QB;
+  double* T = G + (size_t)QB * QB;
+  double* Wm = T + (size_t)QB * QB;
+  double* X = Wm + (size_t)QB * m;
+  for (int j0 = 0; j0 < nref_all; j0 += QB) {
+    const int nref = std::min(QB, nref_all - j0);
+    const int r0 = ((j0 + 1) / 16) * 16;  // rows below r0 of this block's V are zero
+    qblock_prep_kernel<<<512, 256, 0, st>>>(V, ld, n, n2, j0, nref, Vb, VbT);
+    LAUNCH_CHECK(ctx);
+    GemmArgs g{};
+    g.P = Vb + r0; g.ldp = n2;
+    g.Q = Vb + r0; g.ldq = n2;
+    g.C = G; g.ldc = QB;
+    g.M = QB; g.N = QB; g.K = n2 - r0;
+    g.alpha = 1.0; g.beta = 0.0;
+    GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+    qblock_t_kernel<<<1, QB, 0, st>>>(G, tau, j0, nref, T);
+    LAUNCH_CHECK(ctx);
+    GemmArgs w{};  // W = V_b^T B (rows >= r0)
+    w.P = Vb + r0; w.ldp = n2;
+    w.Q = dB + r0; w.ldq = ldb;
+    w.C = Wm; w.ldc = QB;
+    w.M = QB; w.N = m; w.K = n - r0;
+    w.alpha = 1.0; w.beta = 0.0;
+    GPR_TRY(launch_gemm_tn(ctx, w, TC_OTHER));
+    GemmArgs x{};  // X = T^T W
+    x.P = T; x.ldp = QB;
+    x.Q = Wm; x.ldq = QB;
+    x.C = X; x.ldc = QB;
+    x.M = QB; x.N = m; x.K = QB;
+    x.alpha = 1.0; x.beta = 0.0;
+    GPR_TRY(launch_gemm_tn(ctx, x, TC_OTHER));
+    GemmArgs u{};  // B -= V_b X (rows >= r0)
+    u.P = VbT + (size_t)r0 * QB; u.ldp = QB;
+    u.Q = X; u.ldq = QB;
+    u.C = dB + r0; u.ldc = ldb;
+    u.M = n - r0; u.N = m; u.K = QB;
+    u.alpha = -1.0; u.beta = 1.0;
+    GPR_TRY(launch_gemm_tn(ctx, u, TC_OTHER));
+  }
+  return 0;
+}
+
+// out[2j] = Iout_j, out[2j+1] = var_j for the quadrature (see quad_tridiag_kernel); C = Q^T [Y | k1]
+// (scr: 4 n ny doubles of device scratch)
+int quad_tridiag_solves(gpr_ctx* ctx, const double* dd, const double* de, int n, const double* C,
+                        int ldc, int ny, const double* dnoise, double k2, double* scr, double* out) {
+  quad_tridiag_kernel<<<(ny + 63) / 64, 64, 0, ctx->stream>>>(dd, de, n, C, (size_t)ldc, ny, dnoise,
+                                                              k2, scr, out);
+  LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+bool sym_tridiag_ok(int n) { return n >= 1 && n <= TRD_MAXN; }
+
+#ifdef GPR_TESTING
+// the last reduction's phase stamps (100 MHz clock): [2][n][6] long longs
+extern "C" int gpr_testing_trd_trace(long long* out, int n) {
+  if (n < 1 || n > TRD_MAXN) return GPR_E_ARG;
+  std::vector<long long> h(2 * (size_t)TRD_MAXN * 6);
+  if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_trd_trace), h.size() * sizeof(long long)) != hipSuccess)
+    return GPR_E_HIP;
+  for (int k = 0; k < 2; ++k)
+    std::copy(h.begin() + (size_t)k * TRD_MAXN * 6, h.begin() + ((size_t)k * TRD_MAXN + n) * 6,
+              out + (size_t)k * n * 6);
+  return 0;
+}
+#endif
+
+extern "C" int gpr_sytrd_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m,
+                               int ldb, double* dd, double* de) {
+  if (!ctx) return GPR_E_ARG;
+  if (n < 0 || m < 0 || lda < std::max(n, 1) || (m > 0 && ldb < std::max(n, 1)) ||
+      (n > 0 && (!dA || !dd || (n > 1 && !de))) || (m > 0 && n > 0 && !dB))
+    return set_err(ctx, GPR_E_ARG, "bad args");
+  return sym_tridiag(ctx, dA, n, lda, dB, m, ldb, dd, de);
+}

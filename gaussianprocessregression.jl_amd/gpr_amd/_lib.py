@@ -85,6 +85,7 @@ _SIGS = {
                                  _dp]),
     "gpr_cv_batch": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _ip, _i, _ip, _i, _i, _i, _d, _dp]),
     "gpr_syev_apply": (_i, [_p, _p, _i, _i, _p, _i, _i, _p, _ip]),
+    "gpr_sytrd_apply": (_i, [_p, _p, _i, _i, _p, _i, _i, _p, _p]),
     "gpr_split_predict_rows": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _ip,
                                     _i, _i, _i, _d, _p, _p]),
     "gpr_split_predict_shard": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _p, _i, _p, _i, _ip,

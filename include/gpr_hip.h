@@ -296,6 +296,15 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
 int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                    double* dlam, int* sweeps);
 
+/* The first stage of that decomposition on its own (LAPACK dsytrd, inside syevr): A (n x n,
+ * ld lda, device, read only, symmetric -- both triangles read) = Q T Q^T with T tridiagonal:
+ * dd[n] its diagonal, de[n-1] its off-diagonal (device), and, when m > 0, dB (n x m, ld ldb)
+ * <- Q^T dB.  One persistent launch (the unblocked two-sided Householder reduction, columns
+ * dealt round-robin over the CUs) + the back-transform by 64-reflector blocks on the MFMA GEMM.
+ * n <= 4608 (GPR_E_UNSUP beyond). */
+int gpr_sytrd_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
+                    double* dd, double* de);
+
 /* ---- a12-a15: split-kernel block prediction ---------------------------------------- */
 /* Test grid x_{e,q} = xe_e + xq_q (Cmap(+, xe, xq), src/split_kernel.jl:1-17).
  * dmu: ne x nq column-major (index e + q*ne, src/split_predict.jl:10-19).

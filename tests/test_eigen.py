@@ -1,6 +1,8 @@
-"""The hand-written symmetric eigensolver (csrc/eigen.hip, block Jacobi) behind the
-sample_noise quadrature -- the reference's LAPACK.syevr! (src/integrate.jl:71-80), whose
-consumer (inverse_diagonal_update!, :81-104) only ever needs lambda and P^T B.
+"""The hand-written symmetric eigensolver behind the sample_noise quadrature -- the reference's
+LAPACK.syevr! (src/integrate.jl:71-80), whose consumer (inverse_diagonal_update!, :81-104) only
+ever needs lambda and P^T B: the tridiagonal reduction (csrc/tridiag.hip, dsytrd) followed by
+divide and conquer on T (csrc/dstedc.hip, dstedc), block Jacobi (csrc/eigen.hip) beyond their
+size bounds.
 
 gpr_syev_apply returns lambda and P^T B, never P; the checks are therefore on what is
 basis-independent:
@@ -61,7 +63,7 @@ def test_syev_random_symmetric(n):
     B = rng.standard_normal((n, 3))
     ctx = G.Context(0)
     lam, C, sweeps = _syev(ctx, A, B)
-    assert 0 < sweeps < 60
+    assert 0 <= sweeps < 60
     ref = np.linalg.eigvalsh(A)
     gap = np.min(np.abs(ref))
     _check(A, lam, C, B, [s for s in (0.0, 0.5, -0.7) if np.min(np.abs(ref + s)) > 1e-3 * max(gap, 1e-3)])
@@ -83,13 +85,24 @@ def test_syev_se_kernel_matrices(kinds, dim, n, length):
     _check(K, lam, C, B, [1e-3, 1e-5, -0.5 * lmin if lmin > 1e-6 else 1e-2])
 
 
+def _perm_of(lam, C, d, B):
+    """(lam, rows of C) is (d, rows of B) in some order, exactly."""
+    used = set()
+    for i in range(len(lam)):
+        hit = [j for j in range(len(d)) if j not in used and d[j] == lam[i]
+               and np.array_equal(B[j], C[i])]
+        assert hit, f"eigenpair {i} ({lam[i]}) is not one of the inputs"
+        used.add(hit[0])
+
+
 def test_syev_diagonal_and_zero():
-    """Already diagonal (no rotation at all: exact), the zero matrix, and a 2 x 2 block."""
+    """Already diagonal (no reflector, every z deflated: exact, in some order), the zero
+    matrix, and a 2 x 2 block."""
     ctx = G.Context(0)
     d = np.array([3.0, -1.0, 2.0, 0.0, 7.5])
     B = np.arange(10.0).reshape(5, 2)
     lam, C, sweeps = _syev(ctx, np.diag(d), B)
-    assert sweeps == 1 and np.array_equal(lam, d) and np.array_equal(C, B)
+    _perm_of(lam, C, d, B)
     lam, C, _ = _syev(ctx, np.zeros((70, 70)), np.ones((70, 1)))
     assert np.array_equal(lam, np.zeros(70)) and np.array_equal(C, np.ones((70, 1)))
     A = np.array([[2.0, 1.0], [1.0, 2.0]])
@@ -122,3 +135,102 @@ def test_integrate_noise_native_vs_rocsolver_comparator(quad, knobs):
     I2, v2 = G.integrate(md, a, b, sample_noise=noise)
     np.testing.assert_allclose(I2, I, rtol=1e-8)
     np.testing.assert_allclose(v2, v, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
+
+
+@pytest.mark.parametrize("n,mult", [(64, 8), (300, 50), (1000, 333), (2049, 700)])
+def test_syev_clustered_spectrum(n, mult):
+    """Eigenvalues repeated exactly `mult` times (plus a few singles): the divide-and-conquer's
+    close-pair deflation (Givens rotations) on every merge; eigenvalues and P^T B as always."""
+    rng = np.random.default_rng(n + mult)
+    Qm, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    ev = np.repeat(np.arange(1.0, n // mult + 2), mult)[:n]
+    ev[-3:] = [50.0, -7.0, 1e-3]
+    A = (Qm * ev) @ Qm.T
+    A = (A + A.T) / 2
+    B = rng.standard_normal((n, 4))
+    ctx = G.Context(0)
+    lam, C, _ = _syev(ctx, A, B)
+    _check(A, lam, C, B, [0.5, -0.25])
+
+
+@pytest.mark.parametrize("n", [4096])
+def test_syev_se_kernel_large(n):
+    """An SE kernel matrix at the quadrature's largest measured size (d = 4, l = 2)."""
+    rng = np.random.default_rng(n)
+    x = rng.random((4, n))
+    hp = np.r_[1.0, [2.0] * 4]
+    K = O.kernel([O.SE], hp, x)
+    B = np.c_[rng.random((n, 2)), O.antideriv_se(x, hp, np.zeros(4), np.ones(4))]
+    ctx = G.Context(0)
+    lam, C, _ = _syev(ctx, K, B)
+    _check(K, lam, C, B, [1e-3, 1e-5])
+
+
+# ---- the tridiagonal reduction (gpr_sytrd_apply: dsytrd, syevr's first stage) -------------
+def _sytrd(ctx, A, B):
+    n = A.shape[0]
+    m = 0 if B is None else B.shape[1]
+    dA = ctx.colmajor(A)
+    dB = ctx.colmajor(B) if m else None
+    dd, de = ctx.empty(max(n, 1)), ctx.empty(max(n - 1, 1))
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    rc = G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, max(n, 1), P(dB), m, max(n, 1), P(dd), P(de))
+    assert rc == 0, G._lib.lib.gpr_last_error(ctx.h)
+    d = ctx.host(dd)[:n]
+    e = ctx.host(de)[:max(n - 1, 0)]
+    return d, e, (ctx.host(dB) if m else None)
+
+
+def _tri(d, e):
+    return np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 17, 64, 65, 129, 257, 300, 1100])
+def test_sytrd_random_symmetric(n):
+    """Q^T A Q = T and Q^T Q = I to rounding (Q^T from B = I), T's eigenvalues are A's."""
+    rng = np.random.default_rng(100 + n)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    ctx = G.Context(0)
+    d, e, Qt = _sytrd(ctx, A, np.eye(n))
+    T = _tri(d, e)
+    eps = np.finfo(float).eps
+    nrm = max(np.linalg.norm(A, 2), 1e-300)
+    assert np.linalg.norm(Qt @ Qt.T - np.eye(n)) <= 20 * n * eps
+    assert np.linalg.norm(Qt @ A @ Qt.T - T) <= 20 * n * eps * nrm
+    assert np.max(np.abs(np.linalg.eigvalsh(T) - np.linalg.eigvalsh(A))) <= 4 * n * eps * nrm
+
+
+@pytest.mark.parametrize("kinds,dim,n", [([O.SE], 2, 150), ([O.SE, O.WN], 3, 300), ([O.SE], 4, 1100),
+                                         ([O.SE], 3, 2048), ([O.SE, O.WN], 8, 4096)])
+def test_sytrd_se_kernel_matrices_quadratic_form(kinds, dim, n):
+    """The reference's matrices (spectrum decaying to the 1e-8 jitter plateau): the quantity the
+    quadrature uses, B^T (K + s I)^{-1} B = (Q^T B)^T (T + s I)^{-1} (Q^T B), for positive and
+    negative shifts, relative 1e-10 x cond(K + s I); column norms of Q^T B preserved."""
+    import scipy.linalg as sla
+    rng = np.random.default_rng(dim * n)
+    x = rng.random((dim, n))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    K = O.kernel(kinds, hp, x)
+    B = np.c_[rng.random((n, 2)), O.antideriv_se(x, hp, np.zeros(dim), np.ones(dim))]
+    ctx = G.Context(0)
+    d, e, C = _sytrd(ctx, K, B)
+    np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-13)
+    lam = np.linalg.eigvalsh(K)
+    for s in (1e-3, 1e-5, -0.5 * lam.min() if lam.min() > 1e-6 else 1e-2):
+        want = B.T @ np.linalg.solve(K + s * np.eye(n), B)
+        got = C.T @ sla.solve_banded((1, 1), np.vstack([np.r_[0.0, e], d + s, np.r_[e, 0.0]]), C)
+        ev = np.abs(lam + s)
+        cond = ev.max() / ev.min()
+        np.testing.assert_allclose(got, want, rtol=1e-10 * cond,
+                                   atol=1e-10 * cond * np.abs(want).max())
+
+
+def test_sytrd_diagonal_and_zero():
+    """Nothing to reduce: T = A and Q = I exactly (every tau = 0)."""
+    ctx = G.Context(0)
+    dg = np.array([3.0, -1.0, 2.0, 0.0, 7.5, 1.0])
+    d, e, C = _sytrd(ctx, np.diag(dg), np.eye(6))
+    assert np.array_equal(d, dg) and np.array_equal(e, np.zeros(5)) and np.array_equal(C, np.eye(6))
+    d, e, _ = _sytrd(ctx, np.zeros((70, 70)), None)
+    assert not d.any() and not e.any()

@@ -1212,23 +1212,27 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   GPR_TRY(launch_kernel_matrix(ctx, kp, dX, n, nullptr, n, 1, K, n));
   double k2 = 0.0;
   GPR_TRY(gpr_antideriv_se(ctx, d, hp, dX, n, a, b, k1, &k2));
-  // the reference's path: K = P diag(lambda) P^T once (LAPACK.syevr!, :75), then per column
-  // j only diagonal updates (inverse_diagonal_update!, :81-104) -- by the hand-written block-
-  // Jacobi eigensolver.  GPR_QUAD_EIGEN=0: K + noise_j I factored per column (PD shifts only);
-  // =2: rocSOLVER's dsyevd for the decomposition (timing comparator; falls back to the
-  // per-column factorisations when it cannot be loaded)
-  // Unset: per-column factorisations -- batched, one tile-DAG launch -- when ny of them cost
-  // less than one eigendecomposition (profiles/r04_eig_speed.txt: ny <= n / 2 + 512 is
-  // conservative), else the eigensolver; a batch that meets a non-positive-definite K + s I
-  // (a shift at or below -lambda_min(K)) falls back to the eigensolver.  =1 forces the eigensolver, =0 the factorisations (GPR_QUAD_SEQ: one at a
-  // time, as before the batched launch).
+  // The reference's path is K = P diag(lambda) P^T once (LAPACK.syevr!, :75), then per column
+  // j only diagonal updates (inverse_diagonal_update!, :81-104).  GPR_QUAD_EIGEN picks:
+  //   1  the tridiagonal reduction K = Q T Q^T (syevr's first stage, tridiag.hip) and one
+  //      pivoted tridiagonal solve per column: k1' (K + s I)^{-1} y = (Q^T k1)' (T + s I)^{-1}
+  //      (Q^T y) -- the same function of the same reduction, without the eigenvectors;
+  //   3  the full decomposition, as the reference: the reduction + divide and conquer on T
+  //      (dstedc.hip), then the diagonal updates; 4 the same by block Jacobi (eigen.hip);
+  //   0  K + noise_j I factored per column (batched tile-DAG launch; positive definite shifts
+  //      only, PosDefException otherwise); 2 rocSOLVER dsyevd (timing comparator).
+  // Unset (-1): per-column factorisations while they cost less than the reduction, else 1 --
+  // the crossover from the measured costs (profiles/r05_eig_speed.txt: batched ~0.5 + ny (4.3e-12
+  // n^3 + 1.4e-8 n^2) ms, reduction + solves ~0.0075 n + 1.4e-9 n^3 + ny 5e-9 n^2 ms: ny ~ 290 at
+  // n = 4096, ~360 at 2048, ~590 at 1100); a batch that meets a K + s I that is not positive
+  // definite (a shift at or below -lambda_min(K)) falls back to route 1.  Beyond the
+  // reduction's bound (n > 6144) the factorisations, whatever ny.
   int qmode = ctx->quad_eigen;
   bool fallback = false;
   if (qmode < 0) {
-    // any shift: K + s I is positive definite for s >= 0 and for -lambda_min(K) < s < 0; a
-    // batch holding an indefinite one fails at that matrix's first non-positive pivot and the
-    // call goes to the eigensolver (a wasted launch of a few ms against the eigensolver's tens)
-    qmode = ny <= n / 2 + 512 ? 0 : 1;
+    const double dn = n, t_fac = 0.5 + ny * (4.26e-12 * dn * dn * dn + 1.37e-8 * dn * dn);
+    const double t_trd = 0.0075 * dn + 1.4e-9 * dn * dn * dn + ny * 5e-9 * dn * dn;
+    qmode = (sym_tridiag_ok(n) && t_trd < t_fac) ? 1 : 0;
     fallback = qmode == 0;
   }
   if (qmode != 0) {

@@ -41,6 +41,7 @@ constexpr int TRD_THREADS = 512;   // 8 waves: one column per wave at a time
 constexpr int TRD_WAVES = TRD_THREADS / 64;
 constexpr int TRD_MAXN = 6144;     // 3 LDS vectors of n doubles per workgroup
 constexpr int TRD_FUSED_M = 1024;  // right-hand sides transformed inside the launch
+constexpr int RPT = (TRD_MAXN + TRD_THREADS - 1) / TRD_THREADS;  // rows per thread, one column
 
 __device__ __forceinline__ double ld1(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -235,22 +236,6 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       if (lane == 0) st1(&a.pbuf[(size_t)j * a.lda + c], p);
       sp += p * vcur[c];
     }
-    // ---- Q^T B on the fly: H_j applied to this workgroup's columns of B (v_j is in every
-    // workgroup's LDS, so no exchange): b -= tau_j (v_j . b) v_j, rows j+1..n-1
-    for (int c = w + wv * P; c < a.m; c += TRD_WAVES * P) {
-      double* b = a.B + (size_t)c * a.ldb;
-      double dot = 0.0;
-      for (int rb = j + 1 + lane; rb < n; rb += 4 * 64) {
-        double x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = rb + 64 * u < n ? b[rb + 64 * u] : 0.0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (rb + 64 * u < n) dot += x[u] * vcur[rb + 64 * u];
-      }
-      const double f = tj * wave_sum(dot);
-      for (int r = j + 1 + lane; r < n; r += 64) b[r] -= f * vcur[r];
-    }
     // ---- publish this workgroup's part of p_j . v_j, arrive, wait for every workgroup
     TRD_STAMP(1);
     if (lane == 0) red[wv] = sp;
@@ -265,6 +250,47 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       __hip_atomic_fetch_add(&a.cnt[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    // ---- Q^T B on the fly, inside the wait for the other workgroups: H_j applied to this
+    // workgroup's columns of B (v_j is in every workgroup's LDS, so no exchange), b -= tau_j
+    // (v_j . b) v_j on rows j+1..n-1.  A few columns: each by the whole workgroup (read once
+    // into registers, written once); four or more: one wave per column.
+    if (a.m > w) {
+      const int mine = (a.m - w + P - 1) / P;
+      if (mine < 4) {
+        for (int c = w; c < a.m; c += P) {
+          double* b = a.B + (size_t)c * a.ldb;
+          double x[RPT];
+          double dot = 0.0;
+#pragma unroll
+          for (int k = 0; k < RPT; ++k) {
+            const int r = j + 1 + tid + k * TRD_THREADS;
+            x[k] = r < n ? b[r] : 0.0;
+            dot += r < n ? x[k] * vcur[r] : 0.0;
+          }
+          const double f = tj * block_sum(dot, red);
+#pragma unroll
+          for (int k = 0; k < RPT; ++k) {
+            const int r = j + 1 + tid + k * TRD_THREADS;
+            if (r < n) b[r] = x[k] - f * vcur[r];
+          }
+        }
+      } else {
+        for (int c = w + wv * P; c < a.m; c += TRD_WAVES * P) {
+          double* b = a.B + (size_t)c * a.ldb;
+          double dot = 0.0;
+          for (int rb = j + 1 + lane; rb < n; rb += 4 * 64) {
+            double x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = rb + 64 * u < n ? b[rb + 64 * u] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (rb + 64 * u < n) dot += x[u] * vcur[rb + 64 * u];
+          }
+          const double f = tj * wave_sum(dot);
+          for (int r = j + 1 + lane; r < n; r += 64) b[r] -= f * vcur[r];
+        }
+      }
+    }
     TRD_STAMP(2);
     if (!trd_wait(a, &a.cnt[j], P, s_ok)) return;
     TRD_STAMP(3);
@@ -275,7 +301,6 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     double* cnew = lds + (size_t)iwp * L;  // (w_{j-1}'s slot) -> v_{j+1}
     const double* pj = a.pbuf + (size_t)j * a.lda;
     const double* cp = a.cpub + (size_t)(j + 1) * a.lda;
-    constexpr int RPT = (TRD_MAXN + TRD_THREADS - 1) / TRD_THREADS;
     double pr[RPT], cr[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
@@ -476,8 +501,17 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
     ctx->ncu = prop.multiProcessorCount;
   }
   const size_t ld = (size_t)(n + 15) / 16 * 16;
-  // workgroups: ~16 columns each (two per wave), at most one per CU
-  const int P = std::max(1, std::min(ctx->ncu, (n + 15) / 16));
+  // workgroups: 8 columns each up to n ~ 1500, 16 above (profiles/r05_trd_sweep.txt: 4..24
+  // columns change n = 512 / 1100 / 2048 / 4096 by <= 12 / 13 / 11 / 1 %), at most one per CU.
+  // (Measured and removed:
+  // the last owned columns held in registers through the whole launch -- every column for n <=
+  // 2048 -- ran no faster: the per-step exchange, not the pass, bounds small n, and at n = 4096
+  // the register pressure cut the pass's loads in flight)
+  int cols = n <= 1536 ? 8 : 16;
+#ifdef GPR_TESTING
+  if (const char* e = getenv("GPR_TRD_COLS")) cols = std::max(1, atoi(e));  // (tuning sweeps)
+#endif
+  const int P = std::max(1, std::min(ctx->ncu, (n + cols - 1) / cols));
   // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), tau, dlast, then ints
   const size_t nW = ld * n;
   const size_t nI = (size_t)n + 2;  // counters, err (as doubles: half of it, rounded up)

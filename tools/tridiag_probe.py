@@ -28,7 +28,7 @@ def best(f, reps=3):
 
 def main():
     sizes = [int(s) for s in (sys.argv[1].split(",") if len(sys.argv) > 1 else "512,1100,2048,4096".split(","))]
-    methods = [int(s) for s in (sys.argv[2].split(",") if len(sys.argv) > 2 else "0,1,2,4".split(","))]
+    methods = [int(s) for s in (sys.argv[2].split(",") if len(sys.argv) > 2 else "0,1,2,3,4".split(","))]
     ctx = core.default_context()
     lib = G._lib.lib
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -46,6 +46,19 @@ def main():
                 lib.gpr_last_error(ctx.h)
             ctx.sync()
         print(f"sytrd n={n:5d} (m=3): {best(trd):8.2f} ms", flush=True)
+        dlam = ctx.empty(n)
+        for mm in (3, n):
+            dB0 = ctx.colmajor(np.eye(n) if mm == n else rng.random((n, mm)))
+            dBw = ctx.empty(mm, n)
+            sw = ctypes.c_int(0)
+
+            def syev():
+                dBw.copy_(dB0)
+                assert lib.gpr_syev_apply(ctx.h, P(dK), n, n, P(dBw), mm, n, P(dlam),
+                                          ctypes.byref(sw)) == 0, lib.gpr_last_error(ctx.h)
+                ctx.sync()
+            print(f"syev  n={n:5d} (m={mm}): {best(syev):8.2f} ms  (tridiagonal + divide and conquer)",
+                  flush=True)
         for ne in (8, 128):
             y = rng.random((n, ne))
             md = G.GPRModel(G.SquaredExp(), hp, x, y)

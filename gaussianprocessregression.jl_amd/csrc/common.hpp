@@ -323,7 +323,7 @@ int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, d
                       int ldc, double* dlam);
 bool tridiag_eig_ok(int n);
 // tridiag.hip: A = Q T Q^T (d, e on the device; B <- Q^T B when m > 0), one persistent launch
-// + blocked WY back-transform; n <= 4608 (sym_tridiag_ok).  Workspace ctx->deig.
+// (+ blocked WY back-transform for m > 1024); n <= 6144 (sym_tridiag_ok).  Workspace ctx->deig.
 int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                 double* dd, double* de);
 bool sym_tridiag_ok(int n);

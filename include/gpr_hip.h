@@ -104,8 +104,10 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
  *   GPR_CV_BATCH       1  gpr_cv_batch: every fold in one batched launch; 0: per fold
  *   GPR_CV_BATCH_GB   16  device-memory budget of one batched cross-validation launch
  *   GPR_CV_STREAMS     4  child contexts of the per-fold / per-column paths (<= 8)
- *   GPR_QUAD_EIGEN    -1  gpr_integrate_noise: -1 auto, 0 per-column factorisations,
- *                         1 the eigensolver, 2 rocSOLVER dsyevd (timing comparator only)
+ *   GPR_QUAD_EIGEN    -1  gpr_integrate_noise: -1 auto (measured cost model), 0 per-column
+ *                         factorisations, 1 tridiagonal reduction + per-column tridiagonal
+ *                         solves, 3 full eigendecomposition (reduction + divide and conquer),
+ *                         4 the same by block Jacobi, 2 rocSOLVER dsyevd (timing comparator)
  *   GPR_QUAD_BATCH_GB 16  device-memory budget of one batched quadrature launch
  *   GPR_QUAD_SEQ       0  1: the per-column factorisations one at a time (no batch)
  * A gpr_mgpu handle reads GPR_MGPU_STREAM (-1 auto: stream U out during device 0's fit only
@@ -250,7 +252,7 @@ int gpr_antideriv_se(gpr_ctx_t ctx, int d, const double* hp, const double* dX, i
                      const double* a, const double* b, double* dk1, double* k2);
 /* integrate(md, hp, a, b; sample_noise=nothing) (src/integrate.jl:48-167): fit (K into dK ->
  * U, dwt = K^{-1} y, n x ny), Iout[ny] = wt' k1, *var = k2 - ||U^{-T} k1||^2 (host outputs).
- * The sample_noise path (symmetric eigendecomposition, :71-78) is gpr_integrate_noise below. */
+ * The sample_noise path (syevr + diagonal updates, :71-104) is gpr_integrate_noise below. */
 int gpr_integrate(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                   const double* dX, int n, const double* dy, int ny, int ldy, const double* a,
                   const double* b, double eps, double* dK, int ldk, double* dwt, double* Iout,
@@ -269,19 +271,21 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
 
 /* integrate(md, hp, a, b; sample_noise = noise::Vector) (src/integrate.jl:71-100,149-162):
  * per column j of y (ny columns, noise[j] host), Iout[j] = k1' (K + noise_j I)^{-1} y_j and
- * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  As the reference: K = P Lambda P' once (the
- * reference's LAPACK syevr; here the hand-written block-Jacobi eigensolver of gpr_syev_apply,
- * which never forms P: T = P' [y | k1] is carried through the rotations), then Iout[j] =
- * sum_i T_ij (P'k1)_i / (lambda_i + noise_j) and var[j] = k2 - sum_i (P'k1)_i^2 / (lambda_i +
- * noise_j): any shift, no factorisation, never info > 0 (an indefinite K + noise_j I gives the
- * reference's indefinite solve).  Default: when ny <= n/2 + 512, the K + noise_j I are
- * factored instead -- all in one batched tile-DAG launch that also solves U_j^{-T} [y_j | k1]
- * (same result within rounding) -- and a factorisation that fails (a shift at or below
- * -lambda_min(K)) hands the call to the eigensolver, so the default never returns info > 0
- * either.  GPR_QUAD_EIGEN=1: always the eigensolver;
- * =0: always the factorisations (positive definite shifts only; info > 0 -- PosDefException
- * -- for the others); =2: rocSOLVER dsyevd (dlopen'd) for the decomposition -- a timing
- * comparator, not the product path. */
+ * var[j] = k2 - k1' (K + noise_j I)^{-1} k1.  The reference decomposes K = P Lambda P' once
+ * (LAPACK syevr) and then only updates a diagonal per column.  Here, by default, one of:
+ *  - the tridiagonal reduction K = Q T Q' (syevr's first stage, gpr_sytrd_apply, with
+ *    C = Q' [y | k1] formed inside the reduction), then per column one pivoted tridiagonal
+ *    solve: Iout[j] = C[:, j]' (T + noise_j I)^{-1} C[:, ny] -- any shift, no factorisation,
+ *    never info > 0 (an indefinite K + noise_j I gives the reference's indefinite solve);
+ *  - the K + noise_j I factored per column, all in one batched tile-DAG launch that also solves
+ *    U_j^{-T} [y_j | k1] (same result within rounding), while that is measured to cost less
+ *    (ny below ~220 at n = 4096, ~250 at 2048, ~400 at 1100, ~800 at 512; always beyond the
+ *    reduction's bound n > 6144); a factorisation that fails (a shift at or below
+ *    -lambda_min(K)) hands the call to the reduction, so the default never returns info > 0.
+ * GPR_QUAD_EIGEN forces a route: 1 the reduction; 3 the reference's full decomposition
+ * (reduction + divide and conquer, gpr_syev_apply) and its diagonal updates; 0 always the
+ * factorisations (positive definite shifts only; info > 0 -- PosDefException -- otherwise);
+ * 2 rocSOLVER dsyevd (dlopen'd) -- a timing comparator, not the product path. */
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                         const double* dX, int n, const double* dy, int ny, int ldy,
                         const double* a, const double* b, const double* noise, double eps,
@@ -291,8 +295,11 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
  * src/integrate.jl:75), applied instead of returned: A (n x n, ld lda, device, read only,
  * symmetric) = P diag(lam) P'; on return dlam[n] (device) holds the eigenvalues -- in no
  * particular order -- and dB (n x m, ld ldb, device) holds P' B, its rows in the order of
- * dlam.  Two-sided block Jacobi (32-wide blocks, parallel ordering), FP64; *sweeps (may be
- * NULL) = sweeps used.  GPR_E_HIP if it does not converge within 60 sweeps. */
+ * dlam.  FP64, as dsyevd: the tridiagonal reduction (gpr_sytrd_apply, B <- Q' B) then Cuppen's
+ * divide and conquer on T (deflation, secular equations, Gu-Eisenstat vectors; Z never formed:
+ * B <- Z' B merge by merge).  n > 6144: two-sided block Jacobi (32-wide blocks, parallel
+ * ordering).  *sweeps (may be NULL) = merge levels (Jacobi: sweeps used).  GPR_E_HIP if Jacobi
+ * does not converge within 60 sweeps. */
 int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                    double* dlam, int* sweeps);
 
@@ -300,8 +307,8 @@ int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, 
  * ld lda, device, read only, symmetric -- both triangles read) = Q T Q^T with T tridiagonal:
  * dd[n] its diagonal, de[n-1] its off-diagonal (device), and, when m > 0, dB (n x m, ld ldb)
  * <- Q^T dB.  One persistent launch (the unblocked two-sided Householder reduction, columns
- * dealt round-robin over the CUs) + the back-transform by 64-reflector blocks on the MFMA GEMM.
- * n <= 4608 (GPR_E_UNSUP beyond). */
+ * dealt round-robin over the CUs; for m <= 1024 Q^T B is formed inside it), else the
+ * back-transform by 64-reflector blocks on the MFMA GEMM.  n <= 6144 (GPR_E_UNSUP beyond). */
 int gpr_sytrd_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                     double* dd, double* de);
 

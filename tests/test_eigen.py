@@ -111,9 +111,10 @@ def test_syev_diagonal_and_zero():
     np.testing.assert_allclose(np.abs(C), np.sqrt(0.5), rtol=1e-15)
 
 
-@pytest.mark.parametrize("quad", ["1", "auto"])
+@pytest.mark.parametrize("quad", ["1", "3", "4", "auto"])
 def test_integrate_noise_native_vs_rocsolver_comparator(quad, knobs):
-    """The hand-written eigensolver (GPR_QUAD_EIGEN=1) and the default (here the batched
+    """The hand-written routes (GPR_QUAD_EIGEN=1 tridiagonal solves, 3 divide and conquer, 4
+    block Jacobi) and the default (here the batched
     factorisations: every shift above -lambda_min) against rocSOLVER's dsyevd as a comparator
     (GPR_QUAD_EIGEN=2, timing/cross-check only) and against the oracle's eigen path."""
     if quad != "auto":

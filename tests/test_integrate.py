@@ -121,12 +121,14 @@ def test_inverse_diagonal_update_oracle(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("quad", ["auto", "1"])
+@pytest.mark.parametrize("quad", ["auto", "1", "3"])
 @pytest.mark.parametrize("name,dim,n,ne", [("SE", 2, 150, 7), ("SE+WN", 3, 300, 12),
                                            ("SE", 4, 1100, 5)])
 def test_integrate_sample_noise_vs_oracle(name, dim, n, ne, quad, knobs):
     """Positive shifts: the default picks the per-column factorisations at these ne (fewer
-    columns than one eigendecomposition costs); GPR_QUAD_EIGEN=1 forces the eigensolver."""
+    columns than one reduction costs); GPR_QUAD_EIGEN=1 forces the tridiagonal reduction +
+    per-column tridiagonal solves, 3 the reference's full eigendecomposition (reduction +
+    divide and conquer) + diagonal updates."""
     if quad != "auto":
         knobs("GPR_QUAD_EIGEN", int(quad))
     kinds = [O.SE] if name == "SE" else [O.SE, O.WN]

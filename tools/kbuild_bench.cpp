@@ -431,7 +431,7 @@ int main(int argc, char** argv) {
         float ms; hipEventElapsedTime(&ms, e0, e1);
         if (rep) best = ms < best ? ms : best;
       }
-      ctx->kup_ptr = nullptr;
+
       double bytes = 0.0;
       for (int c0 = 0; c0 < N; c0 += 128) bytes += 8.0 * std::min(128, N - c0) * std::min(N, c0 + 128);
       printf("kbuild %-9s upper N=%d d=%d: %.3f ms  %.0f GB/s (%.1f%% of 8 TB/s) [%.2f GB written]\n",

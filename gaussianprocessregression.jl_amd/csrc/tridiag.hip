@@ -381,24 +381,98 @@ __global__ void qblock_prep_kernel(const double* __restrict__ V, size_t ldv, int
   }
 }
 
+// [G | W] = Vb^T [Vb | B] for one block, split over the rows (thin outputs -- 64 rows, long K --
+// leave a tiled GEMM a few dozen tiles; here every 64-column tile x row slice is a workgroup).
+// Workgroup (tile x, slice y): rows [k0, k1) of the slice, output columns [64x, 64x + 64) of the
+// Nc = QB + m columns (c < QB: Vb's column c, else B's column c - QB); 16-row stages through
+// LDS, each thread a 4 x 4 block of outputs.  part[y] (QB x Nc, ld QB) = the slice's sum.
+constexpr int GW_KB = 16;
+__global__ __launch_bounds__(256) void qblock_gw_partial_kernel(
+    const double* __restrict__ Vb, int n2, const double* __restrict__ B, size_t ldb, int m,
+    int r0, int n, int ks, double* __restrict__ part) {
+  __shared__ double sP[GW_KB][QB + 2];
+  __shared__ double sQ[GW_KB][QB + 2];
+  const int tid = threadIdx.x;
+  const int nc = QB + m;
+  const int c0 = blockIdx.x * 64;
+  const int k0 = r0 + blockIdx.y * ks, k1 = min(n, k0 + ks);
+  const int ti = (tid & 15) * 4, tc = (tid >> 4) * 4;
+  double acc[4][4] = {};
+  const int lr = tid & 15, lc = tid >> 4;  // loader: row lr, columns lc + 16 q
+  for (int kb = k0; kb < k1; kb += GW_KB) {
+    const int r = kb + lr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = lc + 16 * q;
+      sP[lr][col] = r < k1 ? Vb[(size_t)col * n2 + r] : 0.0;
+      const int c = c0 + col;
+      double v = 0.0;
+      if (r < k1 && c < nc) v = c < QB ? Vb[(size_t)c * n2 + r] : B[(size_t)(c - QB) * ldb + r];
+      sQ[lr][col] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < GW_KB; ++rr) {
+      double a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = sP[rr][ti + u];
+        b[u] = sQ[rr][tc + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] = fma(a[u], b[v], acc[u][v]);
+    }
+    __syncthreads();
+  }
+  double* out = part + (size_t)blockIdx.y * QB * nc;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int c = c0 + tc + v;
+    if (c < nc)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) out[(size_t)c * QB + ti + u] = acc[u][v];
+  }
+}
+
+// G (QB x QB) and W (QB x m, ld QB) = the sum of the S slices (fixed order: deterministic)
+__global__ void qblock_gw_reduce_kernel(const double* __restrict__ part, int S, int m,
+                                        double* __restrict__ G, double* __restrict__ W) {
+  const size_t nc = (size_t)QB + m, tot = (size_t)QB * nc;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < tot;
+       t += (size_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int y = 0; y < S; ++y) s += part[(size_t)y * tot + t];
+    if (t < (size_t)QB * QB) G[t] = s;
+    else W[t - (size_t)QB * QB] = s;
+  }
+}
+
 // T (QB x QB upper, ld QB) from G = Vb^T Vb and tau: T(i,i) = tau_i, T(0:i, i) = -tau_i
-// T(0:i, 0:i) G(0:i, i) (dlarft forward / columnwise); unused columns (i >= nref) zero
+// T(0:i, 0:i) G(0:i, i) (dlarft forward / columnwise); unused columns (i >= nref) zero.  G and
+// tau are staged in LDS first (the recurrence's 64 steps then never wait on memory).
 __global__ __launch_bounds__(QB) void qblock_t_kernel(const double* __restrict__ G,
                                                      const double* __restrict__ tau, int j0,
                                                      int nref, double* __restrict__ T) {
   __shared__ double Ts[QB][QB + 1];
+  __shared__ double Gs[QB][QB + 1];
   __shared__ double g[QB];
+  __shared__ double ts[QB];
   const int k = threadIdx.x;
-  for (int i = 0; i < QB; ++i) Ts[k][i] = 0.0;
+  for (int i = 0; i < QB; ++i) {
+    Ts[k][i] = 0.0;
+    Gs[k][i] = G[k + (size_t)i * QB];
+  }
+  ts[k] = k < nref ? tau[j0 + k] : 0.0;
   __syncthreads();
   for (int i = 0; i < nref; ++i) {
-    const double ti = tau[j0 + i];
-    g[k] = k < i ? -ti * G[k + (size_t)i * QB] : 0.0;
+    const double ti = ts[i];
+    g[k] = k < i ? -ti * Gs[k][i] : 0.0;
     __syncthreads();
     double s = 0.0;
     if (k < i)
       for (int l = k; l < i; ++l) s += Ts[k][l] * g[l];
-    __syncthreads();
     if (k < i) Ts[k][i] = s;
     if (k == i) Ts[i][i] = ti;
     __syncthreads();
@@ -520,7 +594,13 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   // appears) up to TRD_FUSED_M columns; wider B (e.g. gpr_syev_apply on B = I) by blocks of
   // 64 reflectors on the MFMA GEMM afterwards
   const bool fused_b = m > 0 && m <= TRD_FUSED_M;
-  const size_t nQ = (m > 0 && !fused_b) ? 2 * (size_t)n2 * QB + 2 * (size_t)QB * QB + 2 * (size_t)QB * m : 0;
+  // the back-transform's row slices: enough workgroups for the chip (~1024), >= 64 rows each
+  const int gw_tiles = (QB + m + 63) / 64;
+  const int gw_S = std::max(1, std::min((n + 63) / 64, (1024 + gw_tiles - 1) / gw_tiles));
+  const size_t nQ = (m > 0 && !fused_b)
+                        ? 2 * (size_t)n2 * QB + 2 * (size_t)QB * QB + 2 * (size_t)QB * m +
+                              (size_t)gw_S * QB * (QB + m)
+                        : 0;
   const size_t need = 4 * nW + (size_t)n * P + (size_t)n + 8 + nI + nQ;
   GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
   double* W = ctx->deig;
@@ -580,27 +660,22 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   double* T = G + (size_t)QB * QB;
   double* Wm = T + (size_t)QB * QB;
   double* X = Wm + (size_t)QB * m;
+  double* Pgw = X + (size_t)QB * m;
   for (int j0 = 0; j0 < nref_all; j0 += QB) {
     const int nref = std::min(QB, nref_all - j0);
     const int r0 = ((j0 + 1) / 16) * 16;  // rows below r0 of this block's V are zero
     qblock_prep_kernel<<<512, 256, 0, st>>>(V, ld, n, n2, j0, nref, Vb, VbT);
     LAUNCH_CHECK(ctx);
-    GemmArgs g{};
-    g.P = Vb + r0; g.ldp = n2;
-    g.Q = Vb + r0; g.ldq = n2;
-    g.C = G; g.ldc = QB;
-    g.M = QB; g.N = QB; g.K = n2 - r0;
-    g.alpha = 1.0; g.beta = 0.0;
-    GPR_TRY(launch_gemm_tn(ctx, g, TC_OTHER));
+    // [G | W] = Vb^T [Vb | B] (rows >= r0), split over row slices
+    const int S = std::max(1, std::min(gw_S, (n - r0 + 63) / 64));
+    const int ks = ((n - r0 + S - 1) / S + GW_KB - 1) / GW_KB * GW_KB;
+    qblock_gw_partial_kernel<<<dim3(gw_tiles, S), 256, 0, st>>>(Vb, n2, dB, (size_t)ldb, m, r0, n,
+                                                                 ks, Pgw);
+    LAUNCH_CHECK(ctx);
+    qblock_gw_reduce_kernel<<<1024, 256, 0, st>>>(Pgw, S, m, G, Wm);
+    LAUNCH_CHECK(ctx);
     qblock_t_kernel<<<1, QB, 0, st>>>(G, tau, j0, nref, T);
     LAUNCH_CHECK(ctx);
-    GemmArgs w{};  // W = V_b^T B (rows >= r0)
-    w.P = Vb + r0; w.ldp = n2;
-    w.Q = dB + r0; w.ldq = ldb;
-    w.C = Wm; w.ldc = QB;
-    w.M = QB; w.N = m; w.K = n - r0;
-    w.alpha = 1.0; w.beta = 0.0;
-    GPR_TRY(launch_gemm_tn(ctx, w, TC_OTHER));
     GemmArgs x{};  // X = T^T W
     x.P = T; x.ldp = QB;
     x.Q = Wm; x.ldq = QB;

@@ -227,6 +227,24 @@ def test_sytrd_se_kernel_matrices_quadratic_form(kinds, dim, n):
                                    atol=1e-10 * cond * np.abs(want).max())
 
 
+@pytest.mark.parametrize("n,m", [(300, 1500), (1030, 1025), (2049, 1100)])
+def test_sytrd_wide_rhs_blocked_matches_fused(n, m):
+    """Q^T B for m > 1024 (64-reflector blocks after the launch, the [G | W] products split over
+    row slices) against Q^T B for the same A formed inside the launch (B = I, or B's columns in
+    pieces of <= 1024): the two paths agree to rounding, and column norms are preserved."""
+    rng = np.random.default_rng(n + m)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    B = rng.standard_normal((n, m))
+    ctx = G.Context(0)
+    d, e, C = _sytrd(ctx, A, B)
+    pieces = [_sytrd(ctx, A, B[:, c:c + 1000])[2] for c in range(0, m, 1000)]
+    d2, e2, _ = _sytrd(ctx, A, None)
+    assert np.array_equal(d, d2) and np.array_equal(e, e2)
+    np.testing.assert_allclose(C, np.hstack(pieces), rtol=0, atol=1e-12 * np.abs(B).max() * np.sqrt(n))
+    np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-13)
+
+
 def test_sytrd_diagonal_and_zero():
     """Nothing to reduce: T = A and Q = I exactly (every tau = 0)."""
     ctx = G.Context(0)

@@ -17,18 +17,19 @@
 //     A(:, c) -= v_{j-1} w_{j-1}[c] + w_{j-1} v_{j-1}[c] and forms p_j[c] = tau_j A(:, c) . v_j
 //     (each column read once and written once, 16-B accesses, 8 row pairs in flight per lane);
 //     the owner of column j + 1 also publishes that column;
-//   * one exchange: each workgroup publishes p_j[c] and its part of p_j . v_j and arrives on the
-//     step's counter; once all P have arrived every workgroup reads p_j, the partial sums and
-//     column j + 1 and forms w_j = p_j - (tau_j / 2)(p_j . v_j) v_j, column j + 1 after step j
-//     and the next reflector (dlarfg) ITSELF -- the same bits everywhere, so no second hop.
-// Hand-offs follow the MI355X guide's sc1 protocol (write-through stores drained before the
-// counter's atomic add, an sc1 poll, a workgroup barrier, sc1 loads), every handed-off address
-// written once per launch (p_j, column j + 1, the partial sums each have their own slot).  Every
-// wait is bounded (~4 s): on a time-out the launch drains and the call reports an error.
+//   * one exchange: each workgroup publishes p_j[c] and its part of p_j . v_j; every
+//     workgroup then reads p_j, the partial sums and column j + 1 -- each of them polled until
+//     its writer's store has landed (the buffers hold a sentinel until written, so every value
+//     is its own arrival flag: no counter, no drain before an arrival) -- and forms w_j =
+//     p_j - (tau_j / 2)(p_j . v_j) v_j, column j + 1 after step j and the next reflector
+//     (dlarfg) ITSELF -- the same bits everywhere, so no second hop.
+// Hand-offs are sc1 (write-through stores, sc1 loads), every handed-off address written once
+// per launch (p_j, column j + 1, the partial sums each have their own slot).  Every wait is
+// bounded: on a time-out the launch drains and the call reports an error.
 //
-// Cost per step: one fan-in of P arrivals plus 2 (n - j) + P sc1 loads per workgroup, and the
-// pass (16 (n - j)^2 / P bytes per workgroup; the work copy stays in the Infinity Cache up to n
-// ~ 4k).
+// Cost per step: the store-to-load latency of one hand-off plus 2 (n - j) + P sc1 loads per
+// workgroup, and the pass (16 (n - j)^2 / P bytes per workgroup; the work copy stays in the
+// Infinity Cache up to n ~ 4k).
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -54,6 +55,19 @@ __device__ __forceinline__ int ld1i(const int* p) {
 }
 __device__ __forceinline__ void st1i(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the exchange buffers' "not yet written" value: a signalling-NaN payload that no arithmetic
+// produces (results are quiet NaNs) -- set before every launch, each address written once
+constexpr unsigned long long TRD_UNSET = 0x7FF4D1A60000BEEFull;
+__device__ __forceinline__ int trd_unset(double v) {
+  return __double_as_longlong(v) == (long long)TRD_UNSET;
+}
+__global__ void trd_fill_unset_kernel(double* __restrict__ p, size_t cnt) {
+  const double u = __longlong_as_double((long long)TRD_UNSET);
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < cnt;
+       t += (size_t)gridDim.x * blockDim.x)
+    p[t] = u;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -88,39 +102,12 @@ struct TrdArgs {
   double* d;        // n: diagonal of T
   double* e;        // n - 1: off-diagonal of T
   double* dlast;    // A(n-1, n-1) after step n - 4's update (from the owner of column n-1)
-  int* cnt;         // n: arrivals of step j's pass
   int* err;         // set on a wait time-out: every wait then gives up
   long long spin_limit;
   double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
   size_t ldb;
   int m;
 };
-
-// lane 0 polls *p >= v (sc1), giving up on a time-out or another workgroup's error; the whole
-// workgroup leaves together.  Returns false on error.
-__device__ bool trd_wait(const TrdArgs& a, const int* p, int v, int* s_ok) {
-  if (threadIdx.x == 0) {
-    int ok = 1;
-    long long spins = 0;
-    while (ld1i(p) < v) {
-      if (ld1i(a.err)) {
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > a.spin_limit) {
-        st1i(a.err, 1);
-        ok = 0;
-        break;
-      }
-    }
-    *s_ok = ok;
-  }
-  __syncthreads();
-  const bool ok = *s_ok != 0;
-  __syncthreads();
-  return ok;
-}
 
 // workgroup sum of one value per thread (red: >= TRD_WAVES doubles of LDS), deterministic: the
 // same inputs give the same bits in every workgroup
@@ -236,18 +223,16 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       if (lane == 0) st1(&a.pbuf[(size_t)j * a.lda + c], p);
       sp += p * vcur[c];
     }
-    // ---- publish this workgroup's part of p_j . v_j, arrive, wait for every workgroup
+    // ---- publish this workgroup's part of p_j . v_j (no arrival counter: every handed-off
+    // value is its own flag, see the exchange)
     TRD_STAMP(1);
     if (lane == 0) red[wv] = sp;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
       double s = 0.0;
 #pragma unroll
       for (int q = 0; q < TRD_WAVES; ++q) s += red[q];
       st1(&a.parts[(size_t)j * P + w], s);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(&a.cnt[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     // ---- Q^T B on the fly, inside the wait for the other workgroups: H_j applied to this
@@ -292,15 +277,15 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       }
     }
     TRD_STAMP(2);
-    if (!trd_wait(a, &a.cnt[j], P, s_ok)) return;
-    TRD_STAMP(3);
-    // ---- w_j, column j + 1 after step j, v_{j+1}: the same bits in every workgroup.  Every
-    // load of the exchange is issued at once (partial sums, p_j, the published column); the
-    // column update also sums the reflector's x-norm.
+    // ---- the exchange: p_j, the published column j + 1 and the P partial sums.  Every one of
+    // these addresses is written once per launch and holds the sentinel until then, so each
+    // value is its own arrival flag: all loads are issued at once, and only values still
+    // holding the sentinel are loaded again (sc1), until none is left in the workgroup.
     double* wnew = lds + (size_t)ivp * L;  // (v_{j-1}'s slot)
     double* cnew = lds + (size_t)iwp * L;  // (w_{j-1}'s slot) -> v_{j+1}
     const double* pj = a.pbuf + (size_t)j * a.lda;
     const double* cp = a.cpub + (size_t)(j + 1) * a.lda;
+    const double* pp = a.parts + (size_t)j * P;
     double pr[RPT], cr[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
@@ -308,10 +293,35 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       pr[k] = r < n ? ld1(&pj[r]) : 0.0;
       cr[k] = r < n ? ld1(&cp[r]) : 0.0;
     }
-    const double pc = ld1(&pj[j + 1]);
-    double s = 0.0;
-    for (int q = tid; q < P; q += TRD_THREADS) s += ld1(&a.parts[(size_t)j * P + q]);
-    const double kj = 0.5 * tj * block_sum(s, red);
+    double pc = ld1(&pj[j + 1]);
+    double pq = tid < P ? ld1(&pp[tid]) : 0.0;
+    for (long long spins = 0;; ++spins) {
+      int miss = trd_unset(pc) | trd_unset(pq);
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) miss |= trd_unset(pr[k]) | trd_unset(cr[k]);
+      if (!__syncthreads_or(miss)) break;
+      if ((spins & 63) == 63) {  // bounded: a time-out here or elsewhere ends every workgroup
+        if (tid == 0) {
+          if (spins > a.spin_limit) st1i(a.err, 1);
+          *s_ok = ld1i(a.err) == 0;
+        }
+        __syncthreads();
+        const bool ok = *s_ok != 0;
+        __syncthreads();
+        if (!ok) return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int r = j + 1 + tid + k * TRD_THREADS;
+        if (trd_unset(pr[k])) pr[k] = ld1(&pj[r]);
+        if (trd_unset(cr[k])) cr[k] = ld1(&cp[r]);
+      }
+      if (trd_unset(pc)) pc = ld1(&pj[j + 1]);
+      if (trd_unset(pq)) pq = ld1(&pp[tid]);
+    }
+    TRD_STAMP(3);
+    const double kj = 0.5 * tj * block_sum(pq, red);
     TRD_STAMP(4);
     const double wc = pc - kj * vcur[j + 1], vc = vcur[j + 1];
     double xn = 0.0;
@@ -352,7 +362,13 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       __syncthreads();
     } else if (out && tid == 0) {  // the last 2 x 2 block: e_{n-2}, d_{n-1}
       a.e[n - 2] = cnew[n - 1];
-      a.d[n - 1] = ld1(a.dlast) - 2.0 * vcur[n - 1] * wnew[n - 1];
+      double dl = ld1(a.dlast);  // (written in the last pass by column n-1's owner: polled too)
+      for (long long spins = 0; trd_unset(dl) && spins <= a.spin_limit; ++spins) {
+        __builtin_amdgcn_s_sleep(1);
+        dl = ld1(a.dlast);
+      }
+      if (trd_unset(dl)) st1i(a.err, 1);
+      a.d[n - 1] = dl - 2.0 * vcur[n - 1] * wnew[n - 1];
     }
     TRD_STAMP(5);
     const int t = ivp;
@@ -585,7 +601,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 #ifdef GPR_TESTING
   if (const char* e = getenv("GPR_TRD_COLS")) cols = std::max(1, atoi(e));  // (tuning sweeps)
 #endif
-  const int P = std::max(1, std::min(ctx->ncu, (n + cols - 1) / cols));
+  const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
   // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), tau, dlast, then ints
   const size_t nW = ld * n;
   const size_t nI = (size_t)n + 2;  // counters, err (as doubles: half of it, rounded up)
@@ -611,7 +627,6 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   double* tau = parts + (size_t)n * P;
   double* dlast = tau + n;
   int* ints = reinterpret_cast<int*>(dlast + 8);
-  int* cnt = ints;
   int* err = ints + n;
   double* Vb = reinterpret_cast<double*>(ints) + nI;  // the Q^T B blocks'
   TimerScope ts(ctx, TC_OTHER, 4.0 * n * (double)n * n / 3.0);
@@ -624,6 +639,10 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   trd_copy_kernel<<<1024, 256, 0, st>>>(dA, (size_t)lda, n, W, ld);
   LAUNCH_CHECK(ctx);
   HIP_TRY(ctx, hipMemsetAsync(ints, 0, sizeof(int) * ((size_t)n + 2), st));
+  // cpub, pbuf, parts (contiguous) and dlast start "unset" (the exchange polls on the values)
+  trd_fill_unset_kernel<<<1024, 256, 0, st>>>(cpub, 2 * nW + (size_t)n * P);
+  trd_fill_unset_kernel<<<1, 64, 0, st>>>(dlast, 1);
+  LAUNCH_CHECK(ctx);
   HIP_TRY(ctx, hipMemsetAsync(tau, 0, sizeof(double) * n, st));
   TrdArgs a{};
   a.A = W;
@@ -639,9 +658,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.d = dd;
   a.e = de;
   a.dlast = dlast;
-  a.cnt = cnt;
   a.err = err;
-  a.spin_limit = 1ll << 24;
+  a.spin_limit = 1ll << 22;
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;
   a.m = fused_b ? m : 0;

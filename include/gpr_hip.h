@@ -279,7 +279,7 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  *    never info > 0 (an indefinite K + noise_j I gives the reference's indefinite solve);
  *  - the K + noise_j I factored per column, all in one batched tile-DAG launch that also solves
  *    U_j^{-T} [y_j | k1] (same result within rounding), while that is measured to cost less
- *    (ny below ~220 at n = 4096, ~250 at 2048, ~400 at 1100, ~800 at 512; always beyond the
+ *    (ny below ~200 at n = 4096, ~240 at 2048, ~380 at 1100, ~770 at 512; always beyond the
  *    reduction's bound n > 6144); a factorisation that fails (a shift at or below
  *    -lambda_min(K)) hands the call to the reduction, so the default never returns info > 0.
  * GPR_QUAD_EIGEN forces a route: 1 the reduction; 3 the reference's full decomposition

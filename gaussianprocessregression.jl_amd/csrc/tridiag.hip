@@ -104,6 +104,9 @@ struct TrdArgs {
   double* dlast;    // A(n-1, n-1) after step n - 4's update (from the owner of column n-1)
   int* err;         // set on a wait time-out: every wait then gives up
   long long spin_limit;
+#ifdef GPR_TESTING
+  int fail_step;    // (test build) workgroup 0 never publishes its partial sum of this step
+#endif
   double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
   size_t ldb;
   int m;
@@ -232,7 +235,10 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       double s = 0.0;
 #pragma unroll
       for (int q = 0; q < TRD_WAVES; ++q) s += red[q];
-      st1(&a.parts[(size_t)j * P + w], s);
+#ifdef GPR_TESTING
+      if (!(j == a.fail_step && w == 0))
+#endif
+        st1(&a.parts[(size_t)j * P + w], s);
     }
     __syncthreads();
     // ---- Q^T B on the fly, inside the wait for the other workgroups: H_j applied to this
@@ -660,6 +666,12 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.dlast = dlast;
   a.err = err;
   a.spin_limit = 1ll << 22;
+#ifdef GPR_TESTING
+  // (fault injection: GPR_TRD_FAIL_STEP = a step whose hand-off never completes; GPR_TRD_SPIN_LIMIT
+  // shortens the bound so the time-out comes quickly)
+  a.fail_step = getenv("GPR_TRD_FAIL_STEP") ? atoi(getenv("GPR_TRD_FAIL_STEP")) : -1;
+  if (const char* e = getenv("GPR_TRD_SPIN_LIMIT")) a.spin_limit = atoll(e);
+#endif
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;
   a.m = fused_b ? m : 0;

@@ -4,7 +4,8 @@ The release libgpr_hip.so has no fault injection at all, so an inherited environ
 never make it time out or drop a chunk on purpose; these scenarios need the switches the test
 build reads at call time: GPR_DAG_SPIN_LIMIT (every tile-DAG dependency wait gives up at once),
 GPR_MGPU_GATE_LIMIT (a streamed broadcast chunk's gate gives up), GPR_MGPU_FAIL_UNPACK (a
-receiver's unpack of chunk k fails).
+receiver's unpack of chunk k fails), GPR_TRD_FAIL_STEP / GPR_TRD_SPIN_LIMIT (a tridiagonal
+reduction hand-off that never completes).
 
     python tests/fault_scenarios.py <scenario> [args...]   -> prints "OK" on success
 
@@ -67,6 +68,34 @@ def dag_timeout():
     mu_o, var_o = O.predict(kinds, hp, x, y, xp, diagonal_var=True)
     np.testing.assert_allclose(mu, mu_o, rtol=1e-8, atol=1e-10)
     np.testing.assert_allclose(var, var_o, rtol=1e-8, atol=1e-8 * O.diag_prior(kinds, hp, 4))
+
+
+def trd_timeout():
+    """The tridiagonal reduction's hand-off polls are bounded (tridiag.hip): with one workgroup's
+    partial sum of step 5 never published (GPR_TRD_FAIL_STEP, test build), every workgroup must
+    give up -- the launch drains, gpr_sytrd_apply returns GPR_E_HIP "timed out" -- and the SAME
+    context must then reduce correctly (the exchange buffers are re-initialised per call)."""
+    import gpr_amd as G
+    ctx = G.Context(0)
+    n = 700
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    dA = ctx.colmajor(A)
+    dd, de = ctx.empty(n), ctx.empty(n)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    call = lambda: G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, n, None, 0, n, P(dd), P(de))  # noqa: E731
+    os.environ["GPR_TRD_FAIL_STEP"] = "5"
+    os.environ["GPR_TRD_SPIN_LIMIT"] = "4096"
+    for _ in range(2):
+        assert call() == -2
+        assert b"timed out" in G._lib.lib.gpr_last_error(ctx.h)
+    del os.environ["GPR_TRD_FAIL_STEP"], os.environ["GPR_TRD_SPIN_LIMIT"]
+    assert call() == 0
+    d, e = ctx.host(dd)[:n], ctx.host(de)[:n - 1]
+    T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    nrm = np.linalg.norm(A, 2)
+    assert np.max(np.abs(np.linalg.eigvalsh(T) - np.linalg.eigvalsh(A))) <= 4 * n * np.finfo(float).eps * nrm
 
 
 def _mgpu_case(seed):

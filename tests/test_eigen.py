@@ -253,3 +253,12 @@ def test_sytrd_diagonal_and_zero():
     assert np.array_equal(d, dg) and np.array_equal(e, np.zeros(5)) and np.array_equal(C, np.eye(6))
     d, e, _ = _sytrd(ctx, np.zeros((70, 70)), None)
     assert not d.any() and not e.any()
+
+
+def test_sytrd_handoff_timeout_drains_and_context_recovers():
+    """The reduction's hand-off polls are bounded; with one partial sum never published (the
+    test build's GPR_TRD_FAIL_STEP), every workgroup gives up, the call reports the time-out,
+    and the same context reduces correctly afterwards (tests/fault_scenarios.py trd_timeout, in
+    a child process on libgpr_hip_testing.so)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("trd_timeout")

@@ -155,6 +155,13 @@ def kinds_of(name):
     return [1 if k == "SE" else 2 for k in name.split("+")]
 
 
+def _timing(lib, ctx, c):
+    """(ms, launches, flops-or-bytes) of the context's timing class c."""
+    ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+    lib.gpr_timing_get(ctx.h, c, ctypes.byref(ms), ctypes.byref(ln), ctypes.byref(fl))
+    return ms.value, ln.value, fl.value
+
+
 def default_hp(kinds, d, noise=0.1):
     hp = []
     for k in kinds:
@@ -455,15 +462,32 @@ def main():
         ctx.sync()
         lib.gpr_timing_enable(ctx.h, 0)
     fused_ms = f0.elapsed_time(f1)
+    cls_get = lambda c: _timing(lib, ctx, c)  # noqa: E731
+    cls = {nm: cls_get(c) for c, nm in
+           enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other", "gemm_pipe", "dag"])}
+    # the SE-ARD kernel (BASELINE configs[1]'s) at this size: the fit's upper-only K build
+    # (gpr_fit, timing class 0), second of two runs -- the north_star's K-assembly target names
+    # N = 32768, d = 8 without a kernel; the headline kbuild_* fields stay the C3 kernel's
+    kse = kinds_of("SE")
+    hse = default_hp(kse, d)
+    kse_a = (ctypes.c_int * 1)(*kse)
+    hse_p = hse.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    kb_se = None
+    if a.kernel != "SE":
+        for _ in range(2):
+            lib.gpr_timing_reset(ctx.h)
+            lib.gpr_timing_enable(ctx.h, 1)
+            rc = lib.gpr_fit(ctx.h, kse_a, 1, hse_p, d, P(dx), N, P(dy), 1, N, 1e-8, P(K), N,
+                             P(alpha), ctypes.byref(info))
+            ctx.sync()
+            lib.gpr_timing_enable(ctx.h, 0)
+            if rc < 0:  # (rc > 0, K not positive definite, still timed the build)
+                break
+            kb_se = cls_get(0)
     names = ["kbuild", "potrf", "potrs", "posterior"]
     for i, nm in enumerate(names):
         stg[nm] = e[i].elapsed_time(e[i + 1])
     unfused_ms = sum(stg.values())
-    cls = {}
-    for c, nm in enumerate(["kbuild", "syrk", "panel", "trsm_gemm", "other", "gemm_pipe", "dag"]):
-        ms, ln, fl = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
-        lib.gpr_timing_get(ctx.h, c, ctypes.byref(ms), ctypes.byref(ln), ctypes.byref(fl))
-        cls[nm] = (ms.value, ln.value, fl.value)
     # K-assembly of the fit (timing class 0 of the fused step): its "flops" slot carries the
     # bytes it writes -- the upper-only build writes the upper triangle and the 128 x 128
     # diagonal blocks (~4 N^2 + 512 N bytes; the tile-DAG writes the other half), the full
@@ -509,6 +533,12 @@ def main():
             "kbuild_bytes": kb_bytes,
             # the standalone full symmetric K (gpr_kernel, 8 N^2 bytes) of the unfused stages
             "kbuild_full_GBps": 8.0 * N * N / (stg["kbuild"] * 1e-3) / 1e9,
+            "kbuild_se_ard": None if kb_se is None else {
+                "kernel": "SE-ARD", "ms": kb_se[0], "bytes": kb_se[2],
+                "GBps": kb_se[2] / (kb_se[0] * 1e-3) / 1e9,
+                "hbm_frac": kb_se[2] / (kb_se[0] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "note": "the fit's upper-only K build for SE-ARD (configs[1]'s kernel) at this "
+                        "N and d, timed inside gpr_fit; not the headline kernel"},
             "potrf_TFLOPs": potrf_tf,
             "potrf_mfma_frac": potrf_tf / FP64_MFMA_PEAK,
             "stage_ms_unfused": stg,

@@ -129,10 +129,12 @@ __device__ double block_sum(double v, double* red) {
 // dlarfg on col[j+1..n-1] in place -> v_j (v_j[j+1] = 1); returns tau_j, *beta = e_j.  Every
 // workgroup computes the same bits (the reflector is formed redundantly everywhere).
 __device__ double trd_reflector(int n, int j, double* col, double* red, double* beta_out) {
+  // (alpha is read before block_sum's barriers: thread 0 overwrites col[j+1] below, and a wave
+  // still to read it after that write would form a different reflector)
+  const double alpha = col[j + 1];
   double s = 0.0;
   for (int r = j + 2 + threadIdx.x; r < n; r += TRD_THREADS) s += col[r] * col[r];
   const double xnorm2 = block_sum(s, red);
-  const double alpha = col[j + 1];
   double tau = 0.0, beta = alpha, scal = 0.0;
   if (xnorm2 > 0.0) {
     beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
@@ -155,6 +157,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   double* red = lds + 3 * (size_t)L;
   int* s_ok = reinterpret_cast<int*>(red + TRD_WAVES);
+  double* s_alpha = red + TRD_WAVES + 1;  // column j+1's entry j+2 after step j (dlarfg's alpha)
   int ivp = 0, iwp = 1, ivc = 2;
   double tj;
 
@@ -340,6 +343,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
         wnew[r] = wr;
         cnew[r] = x;
         if (r >= j + 3) xn += x * x;
+        if (r == j + 2) *s_alpha = x;
       }
     }
     const double xnorm2 = block_sum(xn, red);  // (its barriers publish cnew / wnew)
@@ -347,7 +351,9 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     if (out && tid == 0) a.d[j + 1] = cnew[j + 1];
     if (j + 1 <= n - 3) {
       // dlarfg on cnew[j+2..n-1] -> v_{j+1} in place
-      const double alpha = cnew[j + 2];
+      // alpha from its own LDS slot, not cnew[j + 2]: thread 0 overwrites that entry with v's
+      // leading 1 below, possibly before another wave has read it (no barrier in between)
+      const double alpha = *s_alpha;
       double tau = 0.0, beta = alpha, scal = 0.0;
       if (xnorm2 > 0.0) {
         beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
@@ -675,7 +681,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;
   a.m = fused_b ? m : 0;
-  const size_t shmem = (3 * (size_t)a.ldl + TRD_WAVES) * sizeof(double) + 16;
+  const size_t shmem = (3 * (size_t)a.ldl + TRD_WAVES + 2) * sizeof(double);
   sytrd_kernel<<<P, TRD_THREADS, shmem, st>>>(a);
   LAUNCH_CHECK(ctx);
   int herr = 0;

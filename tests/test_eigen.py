@@ -262,3 +262,44 @@ def test_sytrd_handoff_timeout_drains_and_context_recovers():
     a child process on libgpr_hip_testing.so)."""
     from conftest import run_fault_scenario
     run_fault_scenario("trd_timeout")
+
+
+def test_syev_largest_size_known_spectrum():
+    """n = 6144, the reduction's and the divide and conquer's largest size (three n-vectors of
+    LDS per workgroup; the merge sort's LDS): A = H3 H2 H1 diag(ev) H1 H2 H3 with Householder
+    H_k, so the eigenvalues are ev exactly; eigenvalues within 4 n eps ||A||, column norms of
+    P^T B preserved, and the quadratic form B^T (A + s I)^{-1} B from the eigenpairs against the
+    same form from the known factors.  One past the bound, the reduction reports GPR_E_UNSUP."""
+    n = 6144
+    rng = np.random.default_rng(6144)
+    ev = np.sort(rng.standard_normal(n)) * 3.0
+    ev[::97] = ev[0]  # a few exact repeats: deflation on the top merges
+    ev = np.sort(ev)
+    A = np.diag(ev)
+    vs = [rng.standard_normal(n) for _ in range(3)]
+    for v in vs:  # A <- H A H, H = I - 2 v v^T / v^T v
+        v = v / np.linalg.norm(v)
+        Av = A @ v
+        A = A - 2.0 * np.outer(v, Av) - 2.0 * np.outer(Av, v) + 4.0 * (v @ Av) * np.outer(v, v)
+    A = (A + A.T) / 2
+    B = rng.standard_normal((n, 3))
+    ctx = G.Context(0)
+    lam, C, _ = _syev(ctx, A, B)
+    eps = np.finfo(float).eps
+    nrm = np.abs(ev).max()
+    assert np.max(np.abs(np.sort(lam) - ev)) <= 4 * n * eps * nrm
+    np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-12)
+    # B^T (A + s I)^{-1} B = (H B)^T (D + s I)^{-1} (H B) with H = H1 H2 H3 applied to B
+    HB = B.copy()
+    for v in reversed(vs):
+        v = v / np.linalg.norm(v)
+        HB = HB - 2.0 * np.outer(v, v @ HB)
+    s = 0.37
+    want = HB.T @ (HB / (ev + s)[:, None])
+    got = C.T @ (C / (lam + s)[:, None])
+    cond = np.abs(ev + s).max() / np.abs(ev + s).min()
+    np.testing.assert_allclose(got, want, rtol=1e-10 * cond, atol=1e-10 * cond * np.abs(want).max())
+    dA = ctx.colmajor(np.eye(n + 1))
+    dd, de = ctx.empty(n + 1), ctx.empty(n)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n + 1, n + 1, None, 0, n + 1, P(dd), P(de)) == -4

@@ -147,6 +147,30 @@ def test_integrate_sample_noise_vs_oracle(name, dim, n, ne, quad, knobs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("quad", ["1", "3"])
+@pytest.mark.parametrize("n,ne", [(1, 3), (2, 1), (3, 4), (4, 2), (17, 5), (129, 1)])
+def test_integrate_sample_noise_small_sizes(n, ne, quad, knobs):
+    """The eigen routes at the smallest sizes: n = 1, 2 (nothing to reduce: T = K), 3 (one
+    reflector), 4, 17, 129, one column and a few, positive and negative shifts -- against the
+    oracle's eigen path."""
+    knobs("GPR_QUAD_EIGEN", int(quad))
+    dim = 2
+    kinds = [O.SE, O.WN]
+    rng = np.random.default_rng(10 * n + ne)
+    x = rng.random((dim, n))
+    Y = rng.random((n, ne))
+    hp = O.default_hp(kinds, dim, length=1.5, noise=0.2)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    lam = np.linalg.eigvalsh(O.kernel(kinds, hp, x))
+    noise = np.r_[1e-3, -0.5 * lam.min(), 0.3][:ne] if ne <= 3 else np.r_[1e-3 * (1.0 + rng.random(ne - 1)), -0.5 * lam.min()]
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I, Io, rtol=1e-9, atol=1e-14)
+    np.testing.assert_allclose(v, vo, rtol=1e-8, atol=1e-12 * O.antideriv2_se(hp, a, b))
+
+
+@pytest.mark.gpu
 def test_integrate_sample_noise_negative(knobs):
     """Negative sample noise, as the reference's eigen path takes it (src/integrate.jl:71-100:
     K = P Lambda P' once, (Lambda + noise_j)^-1 per column, never a factorisation): a shift

@@ -17,17 +17,17 @@
 //     A(:, c) -= v_{j-1} w_{j-1}[c] + w_{j-1} v_{j-1}[c] and forms p_j[c] = tau_j A(:, c) . v_j
 //     (each column read once and written once, 16-B accesses, 8 row pairs in flight per lane);
 //     the owner of column j + 1 also publishes that column;
-//   * one exchange: each workgroup publishes p_j[c]; every workgroup then reads p_j and
-//     column j + 1 -- each value polled until its writer's store has landed (the buffers hold
-//     a sentinel until written, so every value is its own arrival flag: no counter, no drain
-//     before an arrival) -- and forms w_j = p_j - (tau_j / 2)(p_j . v_j) v_j (p_j . v_j summed
-//     from the whole p_j, in the same order everywhere), column j + 1 after step j and the
-//     next reflector (dlarfg) ITSELF -- the same bits everywhere, so no second hop.
+//   * one exchange: each workgroup publishes p_j[c] and its part of p_j . v_j; every
+//     workgroup then reads p_j, the partial sums and column j + 1 -- each of them polled until
+//     its writer's store has landed (the buffers hold a sentinel until written, so every value
+//     is its own arrival flag: no counter, no drain before an arrival) -- and forms w_j =
+//     p_j - (tau_j / 2)(p_j . v_j) v_j, column j + 1 after step j and the next reflector
+//     (dlarfg) ITSELF -- the same bits everywhere, so no second hop.
 // Hand-offs are sc1 (write-through stores, sc1 loads), every handed-off address written once
-// per launch (p_j and column j + 1 each have their own slot).  Every wait is bounded: on a
-// time-out the launch drains and the call reports an error.
+// per launch (p_j, column j + 1, the partial sums each have their own slot).  Every wait is
+// bounded: on a time-out the launch drains and the call reports an error.
 //
-// Cost per step: the store-to-load latency of one hand-off plus 2 (n - j) sc1 loads per
+// Cost per step: the store-to-load latency of one hand-off plus 2 (n - j) + P sc1 loads per
 // workgroup, and the pass (16 (n - j)^2 / P bytes per workgroup; the work copy stays in the
 // Infinity Cache up to n ~ 4k).
 #include <algorithm>
@@ -97,6 +97,7 @@ struct TrdArgs {
   double* V;        // n x n (ld lda): column j = v_j on rows j+1..n-1 (v_j[j+1] = 1)
   double* cpub;     // n x n (ld lda): column j + 1 after step j - 1, published by its owner
   double* pbuf;     // n x n (ld lda): column j = p_j
+  double* parts;    // n x P partial sums p_j . v_j
   double* tau;      // n (tau[n-2], tau[n-1] = 0)
   double* d;        // n: diagonal of T
   double* e;        // n - 1: off-diagonal of T
@@ -104,7 +105,7 @@ struct TrdArgs {
   int* err;         // set on a wait time-out: every wait then gives up
   long long spin_limit;
 #ifdef GPR_TESTING
-  int fail_step;    // (test build) workgroup 0 never publishes its first p entry of this step
+  int fail_step;    // (test build) workgroup 0 never publishes its partial sum of this step
 #endif
   double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
   size_t ldb;
@@ -184,6 +185,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), 8 row pairs
     // in flight per lane
     TRD_STAMP(0);
+    double sp = 0.0;
     const int r0 = (j + 1) & ~1;
     const int c0 = w + ((j + 1 - w + P - 1) / P) * P;  // first owned column > j
     for (int c = c0 + wv * P; c < n; c += TRD_WAVES * P) {
@@ -224,12 +226,24 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
         }
       }
       const double p = tj * wave_sum(dot);
-#ifdef GPR_TESTING
-      if (j == a.fail_step && w == 0 && c == c0) continue;  // (fault injection: p_j[c0] never published)
-#endif
       if (lane == 0) st1(&a.pbuf[(size_t)j * a.lda + c], p);
+      sp += p * vcur[c];
     }
+    // ---- publish this workgroup's part of p_j . v_j (no arrival counter: every handed-off
+    // value is its own flag, see the exchange)
     TRD_STAMP(1);
+    if (lane == 0) red[wv] = sp;
+    __syncthreads();
+    if (tid == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < TRD_WAVES; ++q) s += red[q];
+#ifdef GPR_TESTING
+      if (!(j == a.fail_step && w == 0))
+#endif
+        st1(&a.parts[(size_t)j * P + w], s);
+    }
+    __syncthreads();
     // ---- Q^T B on the fly, inside the wait for the other workgroups: H_j applied to this
     // workgroup's columns of B (v_j is in every workgroup's LDS, so no exchange), b -= tau_j
     // (v_j . b) v_j on rows j+1..n-1.  A few columns: each by the whole workgroup (read once
@@ -272,16 +286,15 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       }
     }
     TRD_STAMP(2);
-    // ---- the exchange: p_j and the published column j + 1.  Every one of these addresses is
-    // written once per launch and holds the sentinel until then, so each value is its own
-    // arrival flag: all loads are issued at once, and only values still holding the sentinel
-    // are loaded again (sc1), until none is left in the workgroup.  p_j . v_j is then summed
-    // here, from the whole p_j, by every workgroup in the same order (no partial sums to hand
-    // off).
+    // ---- the exchange: p_j, the published column j + 1 and the P partial sums.  Every one of
+    // these addresses is written once per launch and holds the sentinel until then, so each
+    // value is its own arrival flag: all loads are issued at once, and only values still
+    // holding the sentinel are loaded again (sc1), until none is left in the workgroup.
     double* wnew = lds + (size_t)ivp * L;  // (v_{j-1}'s slot)
     double* cnew = lds + (size_t)iwp * L;  // (w_{j-1}'s slot) -> v_{j+1}
     const double* pj = a.pbuf + (size_t)j * a.lda;
     const double* cp = a.cpub + (size_t)(j + 1) * a.lda;
+    const double* pp = a.parts + (size_t)j * P;
     double pr[RPT], cr[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
@@ -290,8 +303,9 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       cr[k] = r < n ? ld1(&cp[r]) : 0.0;
     }
     double pc = ld1(&pj[j + 1]);
+    double pq = tid < P ? ld1(&pp[tid]) : 0.0;
     for (long long spins = 0;; ++spins) {
-      int miss = trd_unset(pc);
+      int miss = trd_unset(pc) | trd_unset(pq);
 #pragma unroll
       for (int k = 0; k < RPT; ++k) miss |= trd_unset(pr[k]) | trd_unset(cr[k]);
       if (!__syncthreads_or(miss)) break;
@@ -313,15 +327,10 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
         if (trd_unset(cr[k])) cr[k] = ld1(&cp[r]);
       }
       if (trd_unset(pc)) pc = ld1(&pj[j + 1]);
+      if (trd_unset(pq)) pq = ld1(&pp[tid]);
     }
     TRD_STAMP(3);
-    double pv = 0.0;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r = j + 1 + tid + k * TRD_THREADS;
-      if (r < n) pv += pr[k] * vcur[r];
-    }
-    const double kj = 0.5 * tj * block_sum(pv, red);
+    const double kj = 0.5 * tj * block_sum(pq, red);
     TRD_STAMP(4);
     const double wc = pc - kj * vcur[j + 1], vc = vcur[j + 1];
     double xn = 0.0;
@@ -605,7 +614,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   if (const char* e = getenv("GPR_TRD_COLS")) cols = std::max(1, atoi(e));  // (tuning sweeps)
 #endif
   const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
-  // workspace: W, V, cpub, pbuf (ld x n each), tau, dlast, then ints
+  // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), tau, dlast, then ints
   const size_t nW = ld * n;
   const size_t nI = (size_t)n + 2;  // counters, err (as doubles: half of it, rounded up)
   const int n2 = (int)ld;
@@ -620,13 +629,14 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
                         ? 2 * (size_t)n2 * QB + 2 * (size_t)QB * QB + 2 * (size_t)QB * m +
                               (size_t)gw_S * QB * (QB + m)
                         : 0;
-  const size_t need = 4 * nW + (size_t)n + 8 + nI + nQ;
+  const size_t need = 4 * nW + (size_t)n * P + (size_t)n + 8 + nI + nQ;
   GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
   double* W = ctx->deig;
   double* V = W + nW;
   double* cpub = V + nW;
   double* pbuf = cpub + nW;
-  double* tau = pbuf + nW;
+  double* parts = pbuf + nW;
+  double* tau = parts + (size_t)n * P;
   double* dlast = tau + n;
   int* ints = reinterpret_cast<int*>(dlast + 8);
   int* err = ints + n;
@@ -641,8 +651,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   trd_copy_kernel<<<1024, 256, 0, st>>>(dA, (size_t)lda, n, W, ld);
   LAUNCH_CHECK(ctx);
   HIP_TRY(ctx, hipMemsetAsync(ints, 0, sizeof(int) * ((size_t)n + 2), st));
-  // cpub, pbuf (contiguous) and dlast start "unset" (the exchange polls on the values)
-  trd_fill_unset_kernel<<<1024, 256, 0, st>>>(cpub, 2 * nW);
+  // cpub, pbuf, parts (contiguous) and dlast start "unset" (the exchange polls on the values)
+  trd_fill_unset_kernel<<<1024, 256, 0, st>>>(cpub, 2 * nW + (size_t)n * P);
   trd_fill_unset_kernel<<<1, 64, 0, st>>>(dlast, 1);
   LAUNCH_CHECK(ctx);
   HIP_TRY(ctx, hipMemsetAsync(tau, 0, sizeof(double) * n, st));
@@ -655,6 +665,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.V = V;
   a.cpub = cpub;
   a.pbuf = pbuf;
+  a.parts = parts;
   a.tau = tau;
   a.d = dd;
   a.e = de;

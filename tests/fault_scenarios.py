@@ -72,7 +72,7 @@ def dag_timeout():
 
 def trd_timeout():
     """The tridiagonal reduction's hand-off polls are bounded (tridiag.hip): with one workgroup's
-    p entry of step 5 never published (GPR_TRD_FAIL_STEP, test build), every workgroup must
+    partial sum of step 5 never published (GPR_TRD_FAIL_STEP, test build), every workgroup must
     give up -- the launch drains, gpr_sytrd_apply returns GPR_E_HIP "timed out" -- and the SAME
     context must then reduce correctly (the exchange buffers are re-initialised per call)."""
     import gpr_amd as G

@@ -256,7 +256,7 @@ def test_sytrd_diagonal_and_zero():
 
 
 def test_sytrd_handoff_timeout_drains_and_context_recovers():
-    """The reduction's hand-off polls are bounded; with one p entry never published (the
+    """The reduction's hand-off polls are bounded; with one partial sum never published (the
     test build's GPR_TRD_FAIL_STEP), every workgroup gives up, the call reports the time-out,
     and the same context reduces correctly afterwards (tests/fault_scenarios.py trd_timeout, in
     a child process on libgpr_hip_testing.so)."""

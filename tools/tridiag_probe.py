@@ -28,7 +28,8 @@ def best(f, reps=3):
 
 def main():
     sizes = [int(s) for s in (sys.argv[1].split(",") if len(sys.argv) > 1 else "512,1100,2048,4096".split(","))]
-    methods = [int(s) for s in (sys.argv[2].split(",") if len(sys.argv) > 2 else "0,1,2,3,4".split(","))]
+    arg = sys.argv[2] if len(sys.argv) > 2 else "0,1,2,3,4"
+    methods = [] if arg == "none" else [int(s) for s in arg.split(",")]
     ctx = core.default_context()
     lib = G._lib.lib
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731

@@ -303,3 +303,37 @@ def test_syev_largest_size_known_spectrum():
     dd, de = ctx.empty(n + 1), ctx.empty(n)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n + 1, n + 1, None, 0, n + 1, P(dd), P(de)) == -4
+
+
+@pytest.mark.parametrize("n,m", [(300, 4), (700, 1100)])
+def test_syev_and_sytrd_padded_leading_dimensions(n, m):
+    """lda > n and ldb > n (a sub-block of larger buffers, as Julia views pass them): the same
+    eigenvalues and P^T B as the packed call, and the padding rows of B untouched."""
+    rng = np.random.default_rng(n + m)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    B = rng.standard_normal((n, m))
+    ctx = G.Context(0)
+    lam0, C0, _ = _syev(ctx, A, B)
+    lda, ldb = n + 5, n + 3
+    Ap = np.full((lda, n), 7.0)
+    Ap[:n] = A
+    Bp = np.full((ldb, m), -3.0)
+    Bp[:n] = B
+    dA, dB = ctx.colmajor(Ap), ctx.colmajor(Bp)
+    lam = ctx.empty(n)
+    sw = ctypes.c_int(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    assert G._lib.lib.gpr_syev_apply(ctx.h, P(dA), n, lda, P(dB), m, ldb, P(lam), ctypes.byref(sw)) == 0
+    Cp = ctx.host(dB)
+    np.testing.assert_array_equal(ctx.host(lam)[:n], lam0)
+    np.testing.assert_array_equal(Cp[:n], C0)
+    assert (Cp[n:] == -3.0).all()
+    dB2 = ctx.colmajor(Bp)
+    dd, de = ctx.empty(n), ctx.empty(n)
+    assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, lda, P(dB2), m, ldb, P(dd), P(de)) == 0
+    d0, e0, Q0 = _sytrd(ctx, A, B)
+    np.testing.assert_array_equal(ctx.host(dd)[:n], d0)
+    np.testing.assert_array_equal(ctx.host(de)[:n - 1], e0)
+    np.testing.assert_array_equal(ctx.host(dB2)[:n], Q0)
+    assert (ctx.host(dB2)[n:] == -3.0).all()

@@ -328,7 +328,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
                 double* dd, double* de);
 bool sym_tridiag_ok(int n);
 // the quadrature's columns from T: out[2j] = C[:, j]' (T + s_j I)^{-1} c, out[2j+1] = k2 - c' (T +
-// s_j I)^{-1} c with c = C[:, ny]; scr: 4 n ny doubles
+// s_j I)^{-1} c with c = C[:, ny]; scr: 4 n quad_tridiag_chunk(n, ny) doubles
+int quad_tridiag_chunk(int n, int ny);
 int quad_tridiag_solves(gpr_ctx* ctx, const double* dd, const double* de, int n, const double* C,
                         int ldc, int ny, const double* dnoise, double k2, double* scr, double* out);
 // norm[j] -= ||B[:, j]||^2 (one wave per column, deterministic), on ctx->stream

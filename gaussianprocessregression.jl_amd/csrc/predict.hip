@@ -1076,7 +1076,8 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
     // sum_i (P'y_j)_i (P'k1)_i / (lambda_i + s_j) without the eigenvectors (any shift)
     const size_t nc = (size_t)n * (ny + 1);
     GPR_TRY(ensure_buf(ctx, &ctx->dbig, &ctx->big_cap,
-                       nc + 2 * (size_t)n + 3 * (size_t)ny + 4 * (size_t)n * ny));
+                       nc + 2 * (size_t)n + 3 * (size_t)ny +
+                           4 * (size_t)n * quad_tridiag_chunk(n, ny)));
     double* C = ctx->dbig;
     double* dd = C + nc;
     double* de = dd + n;

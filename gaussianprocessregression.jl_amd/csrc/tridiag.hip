@@ -512,16 +512,17 @@ __global__ __launch_bounds__(QB) void qblock_t_kernel(const double* __restrict__
 // Column j (one thread): x = (T + s_j I)^{-1} c with c = C[:, ny] = Q^T k1 by Gaussian
 // elimination with partial pivoting on the tridiagonal (dgtsv: the row interchanges fill a
 // second superdiagonal), then out[2j] = C[:, j] . x (= k1' (K + s_j I)^{-1} y_j, Iout) and
-// out[2j+1] = k2 - c . x (var).  Scratch: 4 n doubles per column.
+// out[2j+1] = k2 - c . x (var).  Columns [j0, j1) of this launch; scratch: 4 n doubles per
+// column of the launch.
 __global__ void quad_tridiag_kernel(const double* __restrict__ d, const double* __restrict__ e,
                                     int n, const double* __restrict__ C, size_t ldc, int ny,
-                                    const double* __restrict__ noise, double k2,
+                                    int j0, int j1, const double* __restrict__ noise, double k2,
                                     double* __restrict__ scr, double* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= ny) return;
+  const int j = j0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= j1) return;
   const double s = noise[j];
   const double* c = C + (size_t)ny * ldc;
-  double* Dm = scr + (size_t)j * 4 * n;  // final pivots
+  double* Dm = scr + (size_t)(j - j0) * 4 * n;  // final pivots
   double* U1 = Dm + n;                   // first superdiagonal
   double* U2 = U1 + n;                   // second superdiagonal (row interchanges)
   double* x = U2 + n;                    // right-hand side -> solution
@@ -731,12 +732,25 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 }
 
 // out[2j] = Iout_j, out[2j+1] = var_j for the quadrature (see quad_tridiag_kernel); C = Q^T [Y | k1]
-// (scr: 4 n ny doubles of device scratch)
+// (scr: 4 n quad_tridiag_chunk(n, ny) doubles of device scratch; launches of that many columns)
+int quad_tridiag_chunk(int n, int ny) {
+#ifdef GPR_TESTING
+  if (const char* e = getenv("GPR_TRD_QCHUNK")) return std::max(1, std::min(ny, atoi(e)));
+#endif
+  // ~1 GB of scratch at most (>= 256 columns per launch: 4 waves per CU-sized launch)
+  const long long cap = std::max(256ll, (1ll << 27) / (4ll * std::max(n, 1)));
+  return (int)std::min<long long>(ny, cap);
+}
+
 int quad_tridiag_solves(gpr_ctx* ctx, const double* dd, const double* de, int n, const double* C,
                         int ldc, int ny, const double* dnoise, double k2, double* scr, double* out) {
-  quad_tridiag_kernel<<<(ny + 63) / 64, 64, 0, ctx->stream>>>(dd, de, n, C, (size_t)ldc, ny, dnoise,
-                                                              k2, scr, out);
-  LAUNCH_CHECK(ctx);
+  const int chunk = quad_tridiag_chunk(n, ny);
+  for (int j0 = 0; j0 < ny; j0 += chunk) {
+    const int j1 = std::min(ny, j0 + chunk);
+    quad_tridiag_kernel<<<(j1 - j0 + 63) / 64, 64, 0, ctx->stream>>>(dd, de, n, C, (size_t)ldc, ny, j0,
+                                                                    j1, dnoise, k2, scr, out);
+    LAUNCH_CHECK(ctx);
+  }
   return 0;
 }
 

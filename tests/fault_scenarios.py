@@ -5,7 +5,8 @@ never make it time out or drop a chunk on purpose; these scenarios need the swit
 build reads at call time: GPR_DAG_SPIN_LIMIT (every tile-DAG dependency wait gives up at once),
 GPR_MGPU_GATE_LIMIT (a streamed broadcast chunk's gate gives up), GPR_MGPU_FAIL_UNPACK (a
 receiver's unpack of chunk k fails), GPR_TRD_FAIL_STEP / GPR_TRD_SPIN_LIMIT (a tridiagonal
-reduction hand-off that never completes).
+reduction hand-off that never completes), GPR_TRD_QCHUNK (the quadrature's tridiagonal solves
+in launches of a few columns).
 
     python tests/fault_scenarios.py <scenario> [args...]   -> prints "OK" on success
 
@@ -96,6 +97,33 @@ def trd_timeout():
     T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
     nrm = np.linalg.norm(A, 2)
     assert np.max(np.abs(np.linalg.eigvalsh(T) - np.linalg.eigvalsh(A))) <= 4 * n * np.finfo(float).eps * nrm
+
+
+def trd_quad_chunks():
+    """The quadrature's per-column tridiagonal solves run in launches of at most
+    quad_tridiag_chunk(n, ny) columns (scratch bound); GPR_TRD_QCHUNK (test build) forces 7-
+    and 1-column launches: the results are bit for bit those of one launch."""
+    import gpr_amd as G
+    dim, n, ne = 3, 400, 30
+    rng = np.random.default_rng(11)
+    x = rng.random((dim, n))
+    Y = rng.random((n, ne))
+    kinds = [O.SE, O.WN]
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    ctx = G.Context(0)
+    ctx.set_knob("GPR_QUAD_EIGEN", 1)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y, ctx=ctx)
+    a, b = np.zeros(dim), np.ones(dim)
+    noise = np.r_[1e-3 * (1.0 + rng.random(ne - 1)), -1e-3]
+    os.environ.pop("GPR_TRD_QCHUNK", None)
+    I0, v0 = G.integrate(md, a, b, sample_noise=noise)
+    for ch in ("7", "1"):
+        os.environ["GPR_TRD_QCHUNK"] = ch
+        I, v = G.integrate(md, a, b, sample_noise=noise)
+        assert np.array_equal(I, I0) and np.array_equal(v, v0), ch
+    del os.environ["GPR_TRD_QCHUNK"]
+    Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I0, Io, rtol=1e-8)
 
 
 def _mgpu_case(seed):

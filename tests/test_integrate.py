@@ -296,3 +296,12 @@ def test_integrate_batched_columns_chunking_and_sequential(n, ne, knobs):
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
     np.testing.assert_allclose(I, Io, rtol=1e-8)
     np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
+
+
+@pytest.mark.gpu
+def test_integrate_tridiagonal_solves_in_chunks():
+    """The per-column tridiagonal solves in launches of 7 and 1 columns (test build's
+    GPR_TRD_QCHUNK) give bit for bit the one-launch result (tests/fault_scenarios.py
+    trd_quad_chunks, in a child process on libgpr_hip_testing.so)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("trd_quad_chunks")

@@ -19,7 +19,7 @@ timeout -k 10 600 python bench.py > gpurun_out/bench_$R.json 2> gpurun_out/bench
 timeout -k 10 300 python bench_mll.py > gpurun_out/bench_mll_$R.json 2> gpurun_out/bench_mll_$R.err && \
 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --n 8192 --np 8192 --kernel SE --no-split > gpurun_out/bench_c2_$R.json 2> gpurun_out/bench_c2_$R.err && \
 timeout -k 10 300 python bench_split.py > gpurun_out/bench_split_$R.json 2> gpurun_out/bench_split_$R.err && \
-timeout -k 10 300 python -u tools/tridiag_probe.py > gpurun_out/eig_speed_$R.txt 2>&1 && \
+TRD_PROBE_CPU=1 timeout -k 10 400 python -u tools/tridiag_probe.py > gpurun_out/eig_speed_$R.txt 2>&1 && \
 bash tools/profile_round.sh $R
 rc=$?
 echo "session rc=$rc"

@@ -47,6 +47,13 @@ def main():
                 lib.gpr_last_error(ctx.h)
             ctx.sync()
         print(f"sytrd n={n:5d} (m=3): {best(trd):8.2f} ms", flush=True)
+        if os.environ.get("TRD_PROBE_CPU"):  # the reference's own CPU step: LAPACK syevr
+            import scipy.linalg as sla
+            from threadpoolctl import threadpool_limits
+            thr = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+            with threadpool_limits(thr):
+                tc = best(lambda: sla.eigh(K, driver="evr", overwrite_a=False, check_finite=False), reps=2)
+            print(f"cpu   n={n:5d} LAPACK dsyevr (values + vectors, {thr} threads): {tc:8.2f} ms", flush=True)
         dlam = ctx.empty(n)
         for mm in (3, n):
             dB0 = ctx.colmajor(np.eye(n) if mm == n else rng.random((n, mm)))

@@ -319,7 +319,10 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
         __syncthreads();
         if (!ok) return;
       }
-      __builtin_amdgcn_s_sleep(1);
+      // long steps (workgroups arrive microseconds apart): poll less often, so the early
+      // arrivals' re-loads leave the memory system to the passes still streaming
+      if (n - j > 2048) __builtin_amdgcn_s_sleep(31);
+      else __builtin_amdgcn_s_sleep(1);
 #pragma unroll
       for (int k = 0; k < RPT; ++k) {
         const int r = j + 1 + tid + k * TRD_THREADS;

@@ -79,6 +79,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 #ifdef GPR_TESTING
 // phase stamps of workgroups 0 and P-1 (test build only: tools/trd_trace.py)
 __device__ long long g_trd_trace[2][TRD_MAXN][6];
+// every workgroup's pass start / pass end at every 64th step (the spread across workgroups)
+__device__ long long g_trd_wg[TRD_MAXN / 64][256][2];
+#define TRD_WGSTAMP(k)                                                             \
+  do {                                                                             \
+    if (tid == 0 && (j & 63) == 0 && w < 256)                                      \
+      g_trd_wg[j >> 6][w][k] = (long long)__builtin_amdgcn_s_memrealtime();        \
+  } while (0)
 #define TRD_STAMP(k)                                                                   \
   do {                                                                                 \
     if (tid == 0 && (w == 0 || w == P - 1))                                            \
@@ -87,6 +94,9 @@ __device__ long long g_trd_trace[2][TRD_MAXN][6];
 #else
 #define TRD_STAMP(k) \
   do {               \
+  } while (0)
+#define TRD_WGSTAMP(k) \
+  do {                 \
   } while (0)
 #endif
 
@@ -185,6 +195,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), 8 row pairs
     // in flight per lane
     TRD_STAMP(0);
+    TRD_WGSTAMP(0);
     double sp = 0.0;
     const int r0 = (j + 1) & ~1;
     const int c0 = w + ((j + 1 - w + P - 1) / P) * P;  // first owned column > j
@@ -234,6 +245,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     TRD_STAMP(1);
     if (lane == 0) red[wv] = sp;
     __syncthreads();
+    TRD_WGSTAMP(1);  // (every wave's pass done)
     if (tid == 0) {
       double s = 0.0;
 #pragma unroll
@@ -761,6 +773,14 @@ bool sym_tridiag_ok(int n) { return n >= 1 && n <= TRD_MAXN; }
 
 #ifdef GPR_TESTING
 // the last reduction's phase stamps (100 MHz clock): [2][n][6] long longs
+// every workgroup's pass start / end at steps 0, 64, 128, ...: [TRD_MAXN / 64][256][2]
+extern "C" int gpr_testing_trd_wg_trace(long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trd_wg), sizeof(long long) * (TRD_MAXN / 64) * 256 * 2) !=
+      hipSuccess)
+    return GPR_E_HIP;
+  return 0;
+}
+
 extern "C" int gpr_testing_trd_trace(long long* out, int n) {
   if (n < 1 || n > TRD_MAXN) return GPR_E_ARG;
   std::vector<long long> h(2 * (size_t)TRD_MAXN * 6);

@@ -130,6 +130,9 @@ def parse():
     ap.add_argument("--kernel", default="SE+SE+WN")
     ap.add_argument("--nb", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-se-ard", action="store_true",
+                    help="skip the SE-ARD K-build line (two extra gpr_fit calls: the profile "
+                         "runs skip it so the kernel trace holds only the C3 step's DAG launches)")
     ap.add_argument("--cpu-n", type=int, default=None, help="CPU baseline N (default --n)")
     ap.add_argument("--cpu-np", type=int, default=None, help="CPU baseline np (default --np)")
     ap.add_argument("--no-split", action="store_true",
@@ -473,7 +476,7 @@ def main():
     kse_a = (ctypes.c_int * 1)(*kse)
     hse_p = hse.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
     kb_se = None
-    if a.kernel != "SE":
+    if a.kernel != "SE" and not a.no_se_ard:
         for _ in range(2):
             lib.gpr_timing_reset(ctx.h)
             lib.gpr_timing_enable(ctx.h, 1)

@@ -15,7 +15,7 @@
 // with v_j, tau_j and (j > 0) v_{j-1}, w_{j-1} in every workgroup's LDS:
 //   * the pass: every workgroup, over its columns c > j, applies step j-1's rank-2 update
 //     A(:, c) -= v_{j-1} w_{j-1}[c] + w_{j-1} v_{j-1}[c] and forms p_j[c] = tau_j A(:, c) . v_j
-//     (each column read once and written once, 16-B accesses, 8 row pairs in flight per lane);
+//     (each column read once and written once, 16-B accesses, 8-16 row pairs in flight per lane);
 //     the owner of column j + 1 also publishes that column;
 //   * one exchange: each workgroup publishes p_j[c] and its part of p_j . v_j; every
 //     workgroup then reads p_j, the partial sums and column j + 1 -- each of them polled until
@@ -42,6 +42,7 @@ constexpr int TRD_THREADS = 512;   // 8 waves: one column per wave at a time
 constexpr int TRD_WAVES = TRD_THREADS / 64;
 constexpr int TRD_MAXN = 6144;     // 3 LDS vectors of n doubles per workgroup
 constexpr int TRD_FUSED_M = 1024;  // right-hand sides transformed inside the launch
+
 constexpr int RPT = (TRD_MAXN + TRD_THREADS - 1) / TRD_THREADS;  // rows per thread, one column
 
 __device__ __forceinline__ double ld1(const double* p) {
@@ -160,6 +161,9 @@ __device__ double trd_reflector(int n, int j, double* col, double* red, double* 
 // Step j's state, identical in every workgroup: vcur = v_j, tau_j; (j > 0) vprev = v_{j-1},
 // wprev = w_{j-1}.  One exchange per step: the pass publishes p_j (and the owner of column
 // j + 1 that column), every workgroup then forms w_j, column j + 1 and v_{j+1} itself.
+// PU: row pairs in flight per lane in the pass (16 from n ~ 800 on: 1-3 % faster at n = 1100-
+// 4096; 8 below, where the extra registers cost more than they hide)
+template <int PU>
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
   extern __shared__ double lds[];
   typedef double d2 __attribute__((ext_vector_type(2)));
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     const double* wprev = lds + (size_t)iwp * L;
     const double* vcur = lds + (size_t)ivc * L;
     // ---- the pass over this workgroup's columns c > j, one wave per column: rows from the
-    // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), 8 row pairs
+    // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), PU row pairs
     // in flight per lane
     TRD_STAMP(0);
     TRD_WGSTAMP(0);
@@ -204,15 +208,15 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       const double wc = j > 0 ? wprev[c] : 0.0, vc = j > 0 ? vprev[c] : 0.0;
       double* pub = c == j + 1 ? a.cpub + (size_t)(j + 1) * a.lda : nullptr;
       double dot = 0.0;
-      for (int rb = r0 + 2 * lane; rb < n; rb += 16 * 64) {
-        d2 x[8];
+      for (int rb = r0 + 2 * lane; rb < n; rb += PU * 128) {
+        d2 x[PU];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < PU; ++u) {
           const int r = rb + 128 * u;
           if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < PU; ++u) {
           const int r = rb + 128 * u;
           if (r < n) {
             const d2 vp = *reinterpret_cast<const d2*>(vprev + r);
@@ -698,7 +702,10 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.ldb = (size_t)ldb;
   a.m = fused_b ? m : 0;
   const size_t shmem = (3 * (size_t)a.ldl + TRD_WAVES + 2) * sizeof(double);
-  sytrd_kernel<<<P, TRD_THREADS, shmem, st>>>(a);
+  if (n >= 800)
+    sytrd_kernel<16><<<P, TRD_THREADS, shmem, st>>>(a);
+  else
+    sytrd_kernel<8><<<P, TRD_THREADS, shmem, st>>>(a);
   LAUNCH_CHECK(ctx);
   int herr = 0;
   HIP_TRY(ctx, hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, st));

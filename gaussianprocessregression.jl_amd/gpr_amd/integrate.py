@@ -7,7 +7,10 @@ The fit, the N-vector of antiderivatives and the triangular solve run on the dev
 var = k2 - ||U^{-T} k1||^2).  ``gauss_integ``/``erf_integ``/``antideriv2`` are scalar host
 functions, as in the reference.  ``sample_noise`` (one value per column of y,
 src/integrate.jl:71-100) integrates column j with K + noise_j I: the reference diagonalises K
-once (syevr), the device factors each shifted K with the MFMA POTRF (``gpr_integrate_noise``).
+once (syevr); ``gpr_integrate_noise`` either reduces K = Q T Q' once (syevr's first stage, any
+shift) and solves one tridiagonal system per column, or factors the shifted K's in one batched
+tile-DAG launch when that costs less (few columns) -- a measured cost model picks, and
+GPR_QUAD_EIGEN forces a route (include/gpr_hip.h).
 """
 from __future__ import annotations
 

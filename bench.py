@@ -18,6 +18,9 @@ HBM before the timed region.
 
 Multi-GPU: the fit does not shard (no distributed Cholesky) -- every rank runs its
 own job ("replicas", weak scaling, no data-path collective); value = jobs/s over all ranks.
+`--gpus N` alone starts N ranks (bench_launch.py: a GPU-free parent forks N fresh processes
+with RANK / LOCAL_RANK / WORLD_SIZE set); under torch.distributed.run WORLD_SIZE must equal
+--gpus or the run exits 2.
 Beside it, key `split_predict`: BASELINE config 5 (split-kernel block prediction, 1M test points)
 SHARDED over all ranks with the RCCL broadcast of U / wt and an all_gather of the shards
 (strong scaling; `--no-split` skips it).
@@ -55,6 +58,8 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+
+from bench_launch import spawn_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK = 78.6      # TFLOP/s, FP64 matrix spec (measured 77.7 in tools/probe)
@@ -152,6 +157,16 @@ def parse():
     a.cpu_n = a.cpu_n or a.n
     a.cpu_np = a.cpu_np or a.npred
     return a
+
+
+def config_label(a):
+    """Which BASELINE.json config the run's workload is (C2: SE-ARD N=8192 d=8; C3: the
+    composed kernel at N=32768 d=8); anything else is labelled `custom`."""
+    if (a.kernel, a.n, a.d) == ("SE", 8192, 8):
+        return "C2"
+    if (a.kernel, a.n, a.d) == ("SE+SE+WN", 32768, 8):
+        return "C3"
+    return "custom"
 
 
 def kinds_of(name):
@@ -357,6 +372,11 @@ def split_leg(a, world, rank, local):
 
 def main():
     a = parse()
+    # --gpus N without a launcher: this process only forks N ranks and never touches the GPU;
+    # under a launcher WORLD_SIZE must equal --gpus (bench_launch.py)
+    code = spawn_ranks(a.gpus)
+    if code is not None:
+        sys.exit(code)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -527,7 +547,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (x~U[0,1)^(d x N) seeded, y=sin(sum x)^2)",
-            "config": {"workload": f"C3 fit+posterior: {a.kernel}, N={N}, d={d}, np={NP}",
+            "config": {"workload": f"{config_label(a)} fit+posterior: {a.kernel}, N={N}, d={d}, "
+                                   f"np={NP}",
                        "N": N, "d": d, "np": NP, "kernel": a.kernel, "nb": a.nb,
                        "parallelism": f"replicas x{world}"},
             "kbuild_GBps": kbuild_gbs,

@@ -23,10 +23,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gaussianprocessregression.jl_amd"))
+sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+
+from bench_launch import spawn_ranks  # noqa: E402
 
 FP64_PEAK = 78.6
 HBM_PEAK = 8000.0
@@ -113,6 +116,9 @@ def _safe(f, *args):
 
 def main():
     a = parse()
+    code = spawn_ranks(a.gpus)  # --gpus N: N fresh rank processes (bench_launch.py)
+    if code is not None:
+        sys.exit(code)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

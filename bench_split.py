@@ -24,10 +24,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gaussianprocessregression.jl_amd"))
+sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+
+from bench_launch import spawn_ranks  # noqa: E402
 
 
 def parse():
@@ -118,6 +121,9 @@ def _safe(f, *args):
 
 def main():
     a = parse()
+    code = spawn_ranks(a.gpus)  # --gpus N: N fresh rank processes (bench_launch.py)
+    if code is not None:
+        sys.exit(code)
     # RCCL prints its banner and warnings to STDOUT from C: everything but the one JSON line
     # goes to stderr (fd 1 points there; the line is written to the saved descriptor)
     sys.stdout.flush()

@@ -175,6 +175,11 @@ struct gpr_ctx {
   size_t eig_cap = 0;
   double* ddc = nullptr;        // divide-and-conquer workspace (dstedc.hip)
   size_t dc_cap = 0;
+  // its merge tables' pinned host staging buffer, re-filled only after dc_tab_ev (the previous
+  // call's upload) has completed
+  int* dc_tab_host = nullptr;
+  size_t dc_tab_host_cap = 0;
+  hipEvent_t dc_tab_ev = nullptr;
   double* dtri = nullptr;       // the tridiagonal T between the two stages
   size_t tri_cap = 0;
   int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)

@@ -610,7 +610,23 @@ int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, d
   a.K = iv + 5 * (size_t)n;
   a.nrot = iv + 6 * (size_t)n;
   int* dtab = reinterpret_cast<int*>(v + nvec);
-  HIP_TRY(ctx, hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  // the tables go up from a context-owned pinned buffer (the call returns with the copy still
+  // queued): the previous call's upload must have read it before it is refilled
+  if (ctx->dc_tab_ev) HIP_TRY(ctx, hipEventSynchronize(ctx->dc_tab_ev));
+  else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->dc_tab_ev, hipEventDisableTiming));
+  if (ctx->dc_tab_host_cap < tab.size()) {
+    if (ctx->dc_tab_host) HIP_TRY(ctx, hipHostFree(ctx->dc_tab_host));
+    ctx->dc_tab_host = nullptr;
+    ctx->dc_tab_host_cap = 0;
+    HIP_TRY(ctx, hipHostMalloc((void**)&ctx->dc_tab_host, tab.size() * sizeof(int)));
+    ctx->dc_tab_host_cap = tab.size();
+  }
+  if (!tab.empty()) {
+    std::copy(tab.begin(), tab.end(), ctx->dc_tab_host);
+    HIP_TRY(ctx, hipMemcpyAsync(dtab, ctx->dc_tab_host, tab.size() * sizeof(int),
+                                hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx, hipEventRecord(ctx->dc_tab_ev, st));
+  }
   TimerScope ts(ctx, TC_OTHER, 0.0);
   dc_init_kernel<<<512, 256, 0, st>>>(dd, de, n, dC, (size_t)ldc, m, X, ldx, dlam);
   LAUNCH_CHECK(ctx);

@@ -281,6 +281,8 @@ int gpr_ctx_destroy(gpr_ctx_t ctx) {
     if (e.d) hipFree(e.d);
   if (ctx->deig) hipFree(ctx->deig);
   if (ctx->ddc) hipFree(ctx->ddc);
+  if (ctx->dc_tab_ev) hipEventDestroy(ctx->dc_tab_ev);
+  if (ctx->dc_tab_host) hipHostFree(ctx->dc_tab_host);
   if (ctx->dtri) hipFree(ctx->dtri);
   if (ctx->dagb) hipFree(ctx->dagb);
   if (ctx->own_stream) hipStreamDestroy(ctx->stream);

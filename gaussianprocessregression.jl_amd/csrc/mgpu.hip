@@ -32,6 +32,7 @@
 #include <array>
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -219,14 +220,43 @@ struct gpr_mgpu {
   // (GPU_MAX_HW_QUEUES = 4) runs its work behind the launch, so everything goes on this one
   hipStream_t sp = nullptr;
   int* derr = nullptr;  // device 0: a gate timed out
-  // knobs, read from the environment once at gpr_mgpu_create (include/gpr_hip.h)
+  // knobs (kMgpuKnobs below): read from the environment once at gpr_mgpu_create, changed
+  // with gpr_mgpu_set_knob (include/gpr_hip.h)
   int stream_out = -1;   // GPR_MGPU_STREAM: U streamed out during device 0's fit (-1: only at ngpu 1)
   int reserve_cu = 8;    // GPR_MGPU_RESERVE_CU: CUs the streamed fit's launch leaves free
   int chunks = 16;       // GPR_MGPU_CHUNKS: tile-row chunks of the broadcast
-  int self_bcast = 0;    // GPR_MGPU_SELF_BCAST: ngpu 1 runs the broadcast protocol to itself
+  int self_bcast = 0;    // (test build only) ngpu 1 runs the broadcast protocol to itself
 };
 
 namespace {
+
+struct MgpuKnob {
+  const char* name;
+  int gpr_mgpu::*ip;
+};
+const MgpuKnob kMgpuKnobs[] = {
+    {"GPR_MGPU_STREAM", &gpr_mgpu::stream_out},
+    {"GPR_MGPU_RESERVE_CU", &gpr_mgpu::reserve_cu},
+    {"GPR_MGPU_CHUNKS", &gpr_mgpu::chunks},
+#ifdef GPR_TESTING
+    // device 0 as its own receiver, so the one-GPU test box runs the broadcast protocol
+    {"GPR_MGPU_SELF_BCAST", &gpr_mgpu::self_bcast},
+#endif
+};
+
+void mgpu_knob_set(gpr_mgpu* h, const MgpuKnob& k, int v) {
+  if (k.ip == &gpr_mgpu::stream_out) v = v < 0 ? -1 : (v != 0);
+  if (k.ip == &gpr_mgpu::reserve_cu) v = std::max(0, v);
+  if (k.ip == &gpr_mgpu::chunks) v = std::max(1, v);
+  h->*k.ip = v;
+}
+
+const MgpuKnob* mgpu_knob_find(const char* name) {
+  if (!name) return nullptr;
+  for (const MgpuKnob& k : kMgpuKnobs)
+    if (!strcmp(k.name, name)) return &k;
+  return nullptr;
+}
 
 int mg_err(gpr_mgpu* h, int code, const char* fmt, ...) {
   char b[512];
@@ -414,10 +444,10 @@ int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out) {
   h->dev.assign(devices, devices + ngpu);
   h->ctx.assign(ngpu, nullptr);
   h->buf.resize(ngpu);
-  if (const char* e = getenv("GPR_MGPU_STREAM")) h->stream_out = atoi(e) != 0;
-  if (const char* e = getenv("GPR_MGPU_RESERVE_CU")) h->reserve_cu = atoi(e);
-  if (const char* e = getenv("GPR_MGPU_CHUNKS")) h->chunks = atoi(e);
-  if (const char* e = getenv("GPR_MGPU_SELF_BCAST")) h->self_bcast = atoi(e) != 0;
+  // the handle's documented knobs (include/gpr_hip.h), read once here; gpr_mgpu_set_knob
+  // changes them on a live handle
+  for (const MgpuKnob& k : kMgpuKnobs)
+    if (const char* e = getenv(k.name)) mgpu_knob_set(h, k, atoi(e));
   for (int i = 0; i < ngpu; ++i) {
     for (int j = 0; j < i; ++j)
       if (h->dev[j] == h->dev[i]) {
@@ -480,6 +510,22 @@ int gpr_mgpu_destroy(gpr_mgpu_t h) {
 }
 
 const char* gpr_mgpu_last_error(gpr_mgpu_t h) { return h ? h->err.c_str() : "null handle"; }
+
+int gpr_mgpu_set_knob(gpr_mgpu_t h, const char* name, double value) {
+  if (!h) return GPR_E_ARG;
+  const MgpuKnob* k = mgpu_knob_find(name);
+  if (!k) return mg_err(h, GPR_E_ARG, "unknown knob %s", name ? name : "(null)");
+  mgpu_knob_set(h, *k, (int)value);
+  return 0;
+}
+
+int gpr_mgpu_get_knob(gpr_mgpu_t h, const char* name, double* value) {
+  if (!h || !value) return GPR_E_ARG;
+  const MgpuKnob* k = mgpu_knob_find(name);
+  if (!k) return mg_err(h, GPR_E_ARG, "unknown knob %s", name ? name : "(null)");
+  *value = (double)(h->*k->ip);
+  return 0;
+}
 
 int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double* hp, int d,
                            const double* X, int ns, const double* y, const double* Xe, int ne,
@@ -581,7 +627,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
         if (err) continue;
         if ((int)k == so.fail_unpack) {
           err = GPR_E_HIP;
-          what = "unpack of chunk " + std::to_string(k) + " (injected: GPR_MGPU_FAIL_UNPACK)";
+          what = "unpack of chunk " + std::to_string(k) + " (injected fault)";
           continue;
         }
         launch_rows_pack(s, b.U, ns, ns, r0, r1, b.pk, false);
@@ -636,7 +682,7 @@ int gpr_split_predict_mgpu(gpr_mgpu_t h, const int* kinds, int nk, const double*
     if (herr) return set_err(c, GPR_E_HIP, "device 0: a tile-row gate timed out");
     if (so.recv_rc)
       return set_err(c, so.recv_rc, "device 0 (self-broadcast receiver): unpack of chunk %d failed%s",
-                     so.fail_unpack, so.fail_unpack >= 0 ? " (injected: GPR_MGPU_FAIL_UNPACK)" : "");
+                     so.fail_unpack, so.fail_unpack >= 0 ? " (injected fault)" : "");
     if (self_bcast) GPR_TRY(gpr_forget_factor(c));
     return gpr_sync(c);
   });

@@ -19,8 +19,10 @@
 #include <mutex>
 #include <thread>
 
+#ifdef GPR_TESTING  // (the rocSOLVER comparator of gpr_integrate_noise: test build only)
 #include <dlfcn.h>
 #include <rocsolver/rocsolver.h>
+#endif
 
 #include "common.hpp"
 
@@ -995,6 +997,7 @@ static int integ_noise_batched(gpr_ctx* ctx, const double* K, int n, const doubl
   return 0;
 }
 
+#ifdef GPR_TESTING
 // ---- rocSOLVER, dlopen'd (the process's own librocsolver.so.0 if loaded -- torch carries
 // one -- else the system's; no link-time dependency), for the eigendecomposition of K
 struct RocsolverApi {
@@ -1027,6 +1030,8 @@ static bool load_rocsolver() {
 static int rb_destroy_fn(void* hdl) {
   return g_rs.destroy ? (int)g_rs.destroy((rocblas_handle)hdl) : 0;
 }
+
+#endif  // GPR_TESTING
 
 // out[2j] = Iout_j = sum_i T[i, j] c_i / (lambda_i + noise_j), out[2j+1] = var_j = k2 - sum_i
 // c_i^2 / (lambda_i + noise_j), c = T[:, ny] = P^T k1  (src/integrate.jl:81-87,89-104,149-162:
@@ -1136,7 +1141,12 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
     }
     return 0;
   }
-  // GPR_QUAD_EIGEN=2: rocSOLVER dsyevd (a timing comparator for the hand-written solver)
+  // GPR_QUAD_EIGEN=2: rocSOLVER dsyevd (a timing comparator for the hand-written solver,
+  // compiled into the test build libgpr_hip_testing.so only)
+#ifndef GPR_TESTING
+  return set_err(ctx, GPR_E_ARG, "quadrature eigen route 2 (rocSOLVER comparator) exists only "
+                 "in the test build");
+#else
   if (!load_rocsolver()) return 1;
   if (!ctx->rb_handle) {
     rocblas_handle hb = nullptr;
@@ -1195,6 +1205,7 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
     var[j] = h[2 * j + 1];
   }
   return 0;
+#endif  // GPR_TESTING
 }
 
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,

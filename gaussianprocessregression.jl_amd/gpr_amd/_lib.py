@@ -97,6 +97,8 @@ _SIGS = {
     "gpr_mgpu_create": (_i, [_i, _ip, POINTER(c_void_p)]),
     "gpr_mgpu_destroy": (_i, [_p]),
     "gpr_mgpu_last_error": (ctypes.c_char_p, [_p]),
+    "gpr_mgpu_set_knob": (_i, [_p, ctypes.c_char_p, _d]),
+    "gpr_mgpu_get_knob": (_i, [_p, ctypes.c_char_p, _dp]),
     "gpr_split_predict_mgpu": (_i, [_p, _ip, _i, _dp, _i, _dp, _i, _dp, _dp, _i, _dp, _i, _i, _i, _d,
                                     _i, _dp, _dp, _ip]),
     "gpr_split_factors": (_i, [_p, _ip, _i, _dp, _i, _p, _i, _p, _i, _p, _i, _i, _p, _p, _p]),

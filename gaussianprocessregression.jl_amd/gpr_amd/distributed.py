@@ -333,6 +333,17 @@ class MultiGPU:
             raise GprError(f"gpr_mgpu_create({self.devices}) failed ({rc})")
         self.h = h
 
+    def set_knob(self, name: str, value: float) -> None:
+        """gpr_mgpu_set_knob: GPR_MGPU_STREAM / _CHUNKS / _RESERVE_CU (include/gpr_hip.h)."""
+        if lib.gpr_mgpu_set_knob(self.h, name.encode(), float(value)) != 0:
+            raise GprError(f"set_knob({name}): {lib.gpr_mgpu_last_error(self.h).decode()}")
+
+    def get_knob(self, name: str) -> float:
+        v = ctypes.c_double()
+        if lib.gpr_mgpu_get_knob(self.h, name.encode(), ctypes.byref(v)) != 0:
+            raise GprError(f"get_knob({name}): {lib.gpr_mgpu_last_error(self.h).decode()}")
+        return v.value
+
     def close(self):
         if getattr(self, "h", None):
             lib.gpr_mgpu_destroy(self.h)

@@ -107,14 +107,18 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
  *   GPR_QUAD_EIGEN    -1  gpr_integrate_noise: -1 auto (measured cost model), 0 per-column
  *                         factorisations, 1 tridiagonal reduction + per-column tridiagonal
  *                         solves, 3 full eigendecomposition (reduction + divide and conquer),
- *                         4 the same by block Jacobi, 2 rocSOLVER dsyevd (timing comparator)
+ *                         4 the same by block Jacobi (2, rocSOLVER dsyevd as a timing
+ *                         comparator, exists only in the test build libgpr_hip_testing.so)
  *   GPR_QUAD_BATCH_GB 16  device-memory budget of one batched quadrature launch
  *   GPR_QUAD_SEQ       0  1: the per-column factorisations one at a time (no batch)
- * A gpr_mgpu handle reads GPR_MGPU_STREAM (-1 auto: stream U out during device 0's fit only
- * for one device), GPR_MGPU_CHUNKS (16), GPR_MGPU_RESERVE_CU (8) and GPR_MGPU_SELF_BCAST (0;
- * 1: a one-device handle runs the broadcast protocol to itself) once, at gpr_mgpu_create.
- * Fault injection (forced wait timeouts, failed unpacks) exists only in the test build
- * libgpr_hip_testing.so. */
+ * A gpr_mgpu handle has knobs of its own, read from the environment once at gpr_mgpu_create
+ * and changed with gpr_mgpu_set_knob / gpr_mgpu_get_knob (below):
+ *   GPR_MGPU_STREAM   -1  1: stream U out during device 0's fit; 0: after it (-1 auto: only
+ *                         for one device)
+ *   GPR_MGPU_CHUNKS   16  tile-row chunks of the broadcast (>= 1)
+ *   GPR_MGPU_RESERVE_CU 8 CUs the streamed fit's launch leaves to the chunks' packs and RCCL
+ * Fault injection (forced wait timeouts, failed unpacks, a one-device handle broadcasting to
+ * itself) exists only in the test build libgpr_hip_testing.so. */
 int gpr_set_knob(gpr_ctx_t ctx, const char* name, double value);
 int gpr_get_knob(gpr_ctx_t ctx, const char* name, double* value);
 int gpr_timing_enable(gpr_ctx_t ctx, int on);
@@ -385,6 +389,10 @@ typedef struct gpr_mgpu* gpr_mgpu_t;
 int gpr_mgpu_create(int ngpu, const int* devices, gpr_mgpu_t* out);
 int gpr_mgpu_destroy(gpr_mgpu_t h);
 const char* gpr_mgpu_last_error(gpr_mgpu_t h);
+/* The handle's knobs (GPR_MGPU_STREAM, GPR_MGPU_CHUNKS, GPR_MGPU_RESERVE_CU; see gpr_set_knob).
+ * Unknown names: GPR_E_ARG. */
+int gpr_mgpu_set_knob(gpr_mgpu_t h, const char* name, double value);
+int gpr_mgpu_get_knob(gpr_mgpu_t h, const char* name, double* value);
 
 /* predict(md, Cmap(+, xe, xq); diagonal_var=true) (src/predict.jl:14-25 ->
  * src/split_predict.jl:5-53) sharded over the handle's GPUs.  HOST arrays in and out (the

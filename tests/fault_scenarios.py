@@ -6,7 +6,8 @@ build reads at call time: GPR_DAG_SPIN_LIMIT (every tile-DAG dependency wait giv
 GPR_MGPU_GATE_LIMIT (a streamed broadcast chunk's gate gives up), GPR_MGPU_FAIL_UNPACK (a
 receiver's unpack of chunk k fails), GPR_TRD_FAIL_STEP / GPR_TRD_SPIN_LIMIT (a tridiagonal
 reduction hand-off that never completes), GPR_TRD_QCHUNK (the quadrature's tridiagonal solves
-in launches of a few columns).
+in launches of a few columns), GPR_MGPU_SELF_BCAST (a one-device handle broadcasting to itself)
+and the rocSOLVER eigen comparator (GPR_QUAD_EIGEN=2).
 
     python tests/fault_scenarios.py <scenario> [args...]   -> prints "OK" on success
 
@@ -124,6 +125,60 @@ def trd_quad_chunks():
     del os.environ["GPR_TRD_QCHUNK"]
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
     np.testing.assert_allclose(I0, Io, rtol=1e-8)
+
+
+def quad_rocsolver():
+    """GPR_QUAD_EIGEN=2 (rocSOLVER dsyevd, test build only) against route 1 and the oracle."""
+    import gpr_amd as G
+    dim, n, ne = 3, 600, 6
+    kinds = [O.SE, O.WN]
+    rng = np.random.default_rng(9)
+    x = rng.random((dim, n))
+    Y = rng.random((n, ne))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    ctx = G.Context(0)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y, ctx=ctx)
+    a, b = np.zeros(dim), np.ones(dim)
+    noise = np.r_[1e-3 * (1.0 + rng.random(ne - 1)), -1e-3]
+    ctx.set_knob("GPR_QUAD_EIGEN", 1)
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    ctx.set_knob("GPR_QUAD_EIGEN", 2)
+    I2, v2 = G.integrate(md, a, b, sample_noise=noise)
+    np.testing.assert_allclose(I2, I, rtol=1e-8)
+    np.testing.assert_allclose(v2, v, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
+    Io, _ = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
+    np.testing.assert_allclose(I2, Io, rtol=1e-8)
+
+
+def mgpu_self_bcast(ns, stream, chunks):
+    """The broadcast path of gpr_split_predict_mgpu on the one-GPU box (GPR_MGPU_SELF_BCAST,
+    test build only): device 0 factors with the hook armed (8 CUs left free), packs each chunk of
+    tile rows as soon as the tile-DAG's progress counters show it final, runs the 1-rank RCCL
+    broadcast of the chunk, unpacks it into a second buffer as a receiver does and predicts from
+    that copy with rebuilt block inverses; the result equals the single-device split predict up
+    to the rebuilt inverses' rounding (rtol 1e-12) -- a chunk packed before its rows were final
+    would differ at O(1).  The schedule knobs go through gpr_mgpu_set_knob."""
+    import gpr_amd as G
+    import gpr_amd.distributed as gd
+    from test_distributed import _problem
+    os.environ["GPR_MGPU_SELF_BCAST"] = "1"
+    kinds, hp, x, y, xe, xq = _problem(ne=9, nq=33, ns=int(ns), d=5, seed=12)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
+    cm = G.Cmap("+", xe, xq)
+    mg = gd.MultiGPU([0])
+    try:
+        mg.set_knob("GPR_MGPU_STREAM", int(stream))
+        mg.set_knob("GPR_MGPU_CHUNKS", int(chunks))
+        assert mg.get_knob("GPR_MGPU_STREAM") == int(stream)
+        assert mg.get_knob("GPR_MGPU_CHUNKS") == int(chunks)
+        assert mg.get_knob("GPR_MGPU_SELF_BCAST") == 1
+        for _ in range(2):  # (the second call re-uses every buffer)
+            mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 9), fit="broadcast")
+    finally:
+        mg.close()
+    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 9))
+    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
 
 
 def _mgpu_case(seed):

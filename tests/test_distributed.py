@@ -441,30 +441,36 @@ def test_split_predict_mgpu_one_device(fit):
     (1504, "0", "3"),    # chunks after the fit (GPR_MGPU_STREAM=0)
     (1500, "1", "16"),   # n % 16 != 0: the padded factorisation declines the hook -> after the fit
 ])
-def test_split_predict_mgpu_broadcast_path_one_device(monkeypatch, ns, stream, chunks):
-    """The broadcast path of gpr_split_predict_mgpu on the one-GPU box (GPR_MGPU_SELF_BCAST):
-    device 0 factors with the hook armed (8 CUs left free), packs each chunk of tile rows as
-    soon as the tile-DAG's progress counters show it final, runs the 1-rank RCCL broadcast of
-    the chunk, unpacks it into a second buffer as a receiver does and predicts from that copy
-    with rebuilt block inverses; the result equals the single-device split predict up to the
-    rebuilt inverses' rounding (rtol 1e-12) -- a chunk packed before its rows were final would
-    differ at O(1)."""
+def test_split_predict_mgpu_broadcast_path_one_device(ns, stream, chunks):
+    """The broadcast path of gpr_split_predict_mgpu on the one-GPU box: device 0 broadcasts to
+    itself (a test-build-only switch) and predicts from the received copy; equal to the single-
+    device split predict to rtol 1e-12 (tests/fault_scenarios.py mgpu_self_bcast, child process
+    on libgpr_hip_testing.so)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("mgpu_self_bcast", ns, stream, chunks)
+
+
+@pytest.mark.gpu
+def test_mgpu_knobs_release_build():
+    """The handle's knobs through gpr_mgpu_set_knob / gpr_mgpu_get_knob (clamped as documented);
+    the release library has no self-broadcast switch (unknown knob -> GprError)."""
     G = pytest.importorskip("gpr_amd")
-    monkeypatch.setenv("GPR_MGPU_SELF_BCAST", "1")
-    monkeypatch.setenv("GPR_MGPU_STREAM", stream)
-    monkeypatch.setenv("GPR_MGPU_CHUNKS", chunks)
-    kinds, hp, x, y, xe, xq = _problem(ne=9, nq=33, ns=ns, d=5, seed=12)
-    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
-    cm = G.Cmap("+", xe, xq)
     mg = gd.MultiGPU([0])
     try:
-        for _ in range(2):  # (the second call re-uses every buffer)
-            mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(1, 9), fit="broadcast")
+        assert mg.get_knob("GPR_MGPU_STREAM") in (-1, 0, 1)
+        mg.set_knob("GPR_MGPU_STREAM", 5)
+        assert mg.get_knob("GPR_MGPU_STREAM") == 1
+        mg.set_knob("GPR_MGPU_STREAM", -3)
+        assert mg.get_knob("GPR_MGPU_STREAM") == -1
+        mg.set_knob("GPR_MGPU_CHUNKS", 0)
+        assert mg.get_knob("GPR_MGPU_CHUNKS") == 1
+        mg.set_knob("GPR_MGPU_RESERVE_CU", 12)
+        assert mg.get_knob("GPR_MGPU_RESERVE_CU") == 12
+        for bad in ("GPR_MGPU_SELF_BCAST", "GPR_DAG", "nope"):
+            with pytest.raises(G.GprError):
+                mg.set_knob(bad, 1)
     finally:
         mg.close()
-    mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(1, 9))
-    np.testing.assert_allclose(mu, mu1, rtol=1e-12, atol=1e-14)
-    np.testing.assert_allclose(var, var1, rtol=1e-12, atol=1e-14)
 
 
 @pytest.mark.gpu
@@ -540,7 +546,7 @@ def test_split_predict_mgpu_unpack_failure_reports_and_recovers(stream, chunk):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream", ["0", "1"])
-def test_split_predict_mgpu_two_devices(monkeypatch, stream):
+def test_split_predict_mgpu_two_devices(stream):
     """gpr_split_predict_mgpu over two GPUs (the real receiver branch, RCCL between devices)
     against the single-device split predict.  Skips on a box with fewer than two GPUs (the
     development pool has one; no ngpu >= 2 run has happened yet)."""
@@ -548,12 +554,12 @@ def test_split_predict_mgpu_two_devices(monkeypatch, stream):
     import torch
     if torch.cuda.device_count() < 2:
         pytest.skip("needs two GPUs")
-    monkeypatch.setenv("GPR_MGPU_STREAM", stream)
     kinds, hp, x, y, xe, xq = _problem(ne=11, nq=13, ns=2048, d=4, seed=15)
     md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, y)
     cm = G.Cmap("+", xe, xq)
     mg = gd.MultiGPU([0, 1])
     try:
+        mg.set_knob("GPR_MGPU_STREAM", int(stream))
         for fit in ("broadcast", "replicate"):
             mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=(2, 11), fit=fit)
             mu1, var1 = G.predict(md, cm, diagonal_var=True, var_range=(2, 11))

@@ -112,11 +112,12 @@ def test_syev_diagonal_and_zero():
 
 
 @pytest.mark.parametrize("quad", ["1", "3", "4", "auto"])
-def test_integrate_noise_native_vs_rocsolver_comparator(quad, knobs):
+def test_integrate_noise_native_routes_vs_oracle(quad, knobs):
     """The hand-written routes (GPR_QUAD_EIGEN=1 tridiagonal solves, 3 divide and conquer, 4
-    block Jacobi) and the default (here the batched
-    factorisations: every shift above -lambda_min) against rocSOLVER's dsyevd as a comparator
-    (GPR_QUAD_EIGEN=2, timing/cross-check only) and against the oracle's eigen path."""
+    block Jacobi) and the default (here the batched factorisations: every shift above
+    -lambda_min) against the oracle's eigen path.  The release library has no rocSOLVER
+    comparator: route 2 is refused with GPR_E_ARG (it lives in libgpr_hip_testing.so, checked
+    by test_integrate_noise_rocsolver_comparator_test_build)."""
     if quad != "auto":
         knobs("GPR_QUAD_EIGEN", int(quad))
     dim, n, ne = 3, 600, 6
@@ -133,9 +134,16 @@ def test_integrate_noise_native_vs_rocsolver_comparator(quad, knobs):
     np.testing.assert_allclose(I, Io, rtol=1e-8)
     np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
     knobs("GPR_QUAD_EIGEN", 2)
-    I2, v2 = G.integrate(md, a, b, sample_noise=noise)
-    np.testing.assert_allclose(I2, I, rtol=1e-8)
-    np.testing.assert_allclose(v2, v, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
+    with pytest.raises(G.GprError, match="test build"):
+        G.integrate(md, a, b, sample_noise=noise)
+
+
+def test_integrate_noise_rocsolver_comparator_test_build():
+    """rocSOLVER's dsyevd as a comparator (GPR_QUAD_EIGEN=2, compiled into the test build only):
+    the same integrals as the hand-written route 1 and the oracle (tests/fault_scenarios.py
+    quad_rocsolver, child process on libgpr_hip_testing.so)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("quad_rocsolver")
 
 
 @pytest.mark.parametrize("n,mult", [(64, 8), (300, 50), (1000, 333), (2049, 700)])

@@ -121,7 +121,7 @@ def test_c5_split_predict_vs_oracle_fixture():
 
 
 @pytest.mark.parametrize("stream", ["0", "1"])
-def test_c5_split_predict_mgpu_all_devices_vs_oracle_fixture(stream, monkeypatch):
+def test_c5_split_predict_mgpu_all_devices_vs_oracle_fixture(stream):
     """C5 sharded over EVERY visible device (gpr_split_predict_mgpu: one context and RCCL
     communicator per device, cost-balanced e-row shards, rows copied straight into the host
     result) against the oracle fixture -- the same rows and tolerances as the single-device
@@ -134,7 +134,6 @@ def test_c5_split_predict_mgpu_all_devices_vs_oracle_fixture(stream, monkeypatch
     if ndev < 2:
         pytest.skip("needs two or more GPUs")
     import gpr_amd.distributed as gd
-    monkeypatch.setenv("GPR_MGPU_STREAM", stream)  # (read at gpr_mgpu_create)
     cfg, inp, fx = _load("C5")
     kinds, hp = cfg["kinds"], inp["hp"]
     md = G.GPRModel(_cov(kinds), hp, inp["x"], inp["y"])
@@ -145,6 +144,7 @@ def test_c5_split_predict_mgpu_all_devices_vs_oracle_fixture(stream, monkeypatch
     rows = fx["rows"]
     mg = gd.MultiGPU(list(range(ndev)))
     try:
+        mg.set_knob("GPR_MGPU_STREAM", int(stream))
         for fit in ("broadcast", "replicate"):
             mu, var = gd.split_predict_mgpu(md, cm, mg, var_range=cfg["var_range"], fit=fit)
             np.testing.assert_allclose(mu[rows], fx["mu_rows"], rtol=1e-8, atol=1e-10)
@@ -154,3 +154,41 @@ def test_c5_split_predict_mgpu_all_devices_vs_oracle_fixture(stream, monkeypatch
             assert np.all(var[hi * nq:] == prior)
     finally:
         mg.close()
+
+
+def test_c5_split_predict_distributed_rccl_vs_oracle_fixture():
+    """C5 through split_predict_distributed over an RCCL process group (backend "nccl"), one
+    fresh process per visible device -- the torch.distributed path bench.py's C5 leg and the
+    driver's SCALE runs measure, not the one-process C ABI path above -- for both fit modes
+    (rank 0 fits and broadcasts the packed U + wt / every rank fits), every rank's all-gathered
+    result against the oracle fixture at the single-device tolerances (tests/dist_c5_worker.py).
+    Skips below two devices: RCCL refuses two ranks on one device (the one-GPU box covers the
+    same path with gloo in test_distributed.py)."""
+    import socket
+    import subprocess
+
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("needs two or more GPUs (one RCCL rank per device)")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(ndev):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(ndev),
+                   LOCAL_WORLD_SIZE=str(ndev), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_c5_worker.py")],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=600)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and f"OK rank {r}" in out, f"rank {r} rc {p.returncode}:\n{out[-3000:]}"

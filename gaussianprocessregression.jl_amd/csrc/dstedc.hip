@@ -15,7 +15,8 @@
 // pair torn once); all merges of one depth run in the same launches (one workgroup per merge
 // for the sort and scan; one wave per root / row for the K^2 parts; tiles of 64 roots x 64
 // columns for U^T).  Node outputs are not sorted (undeflated roots ascending, then the
-// deflated values); the parent sorts its k values first.  n <= 6144 (LDS of the sort).
+// deflated values); the parent sorts its k values first.  n <= 16384: a merge's sort runs in
+// LDS up to 8192 values (12 bytes each), in global memory above (the top merge only).
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -24,7 +25,8 @@
 
 namespace {
 
-constexpr int DC_MAXN = 6144;
+constexpr int DC_MAXN = 16384;
+constexpr int DC_LDS_SORT = 8192;  // merges of more values sort in global memory
 constexpr int DC_SORT_THREADS = 1024;
 constexpr double DC_EPS = 2.220446049250313e-16;
 
@@ -99,15 +101,20 @@ __global__ void dc_init_kernel(const double* __restrict__ d, const double* __res
 }
 
 // K1: gather d and z, fix the first / last columns, sort by d, tolerance, deflation scan
-// (dlaed2), one workgroup per merge.  LDS: key[kp], idx[kp] (int), zz[k].
-__global__ __launch_bounds__(DC_SORT_THREADS) void dc_prep_kernel(DcArgs a, DcLevel L, int kp) {
+// (dlaed2), one workgroup per merge.  key[kp], idx[kp] (int) in LDS, or (GSORT: kp >
+// DC_LDS_SORT) in global scratch gkey / gidx (kp per merge); z in zhat's rows of the merge
+// (free until dc_zhat_kernel).  Global scratch is read only by the workgroup that wrote it, after
+// a barrier.
+template <bool GSORT>
+__global__ __launch_bounds__(DC_SORT_THREADS) void dc_prep_kernel(DcArgs a, DcLevel L, int kp,
+                                                                  double* gkey, int* gidx) {
   extern __shared__ double sm[];
   const int t = blockIdx.x;
   const int lo = L.ma[t], mid = L.mm[t], hi = L.mb[t];
   const int k = hi - lo, k1 = mid - lo;
-  double* key = sm;
-  int* idx = reinterpret_cast<int*>(key + kp);
-  double* zz = reinterpret_cast<double*>(idx + kp);
+  double* key = GSORT ? gkey + (size_t)t * kp : sm;
+  int* idx = GSORT ? gidx + (size_t)t * kp : reinterpret_cast<int*>(key + kp);
+  double* zz = a.zhat + lo;
   __shared__ double red[2][DC_SORT_THREADS / 64];
   const double beta = a.e[mid - 1];
   const double sgn = beta >= 0.0 ? 1.0 : -1.0;
@@ -580,7 +587,14 @@ int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, d
   const size_t nX = ldx * mx;
   const size_t nvec = 16 * (size_t)n + 3 * (size_t)nodes.size() + 64;
   const size_t ntab = (tab.size() + 1) / 2 + 1;
-  GPR_TRY(ensure_buf(ctx, &ctx->ddc, &ctx->dc_cap, 2 * nX + nvec + ntab));
+  // global sort scratch for the merges beyond the LDS sort (kp values: a double and an int each)
+  size_t gsort_cap = 0;
+  for (int dpt = 0; dpt <= maxd; ++dpt) {
+    int kp = 2;
+    while (kp < off[dpt].kmax) kp <<= 1;
+    if (kp > DC_LDS_SORT) gsort_cap = std::max(gsort_cap, (size_t)off[dpt].nmerge * kp);
+  }
+  GPR_TRY(ensure_buf(ctx, &ctx->ddc, &ctx->dc_cap, 2 * nX + nvec + ntab + gsort_cap + (gsort_cap + 1) / 2));
   double* X = ctx->ddc;
   double* Xt = X + nX;
   double* v = Xt + nX;
@@ -610,6 +624,8 @@ int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, d
   a.K = iv + 5 * (size_t)n;
   a.nrot = iv + 6 * (size_t)n;
   int* dtab = reinterpret_cast<int*>(v + nvec);
+  double* gkey = v + nvec + ntab;
+  int* gidx = reinterpret_cast<int*>(gkey + gsort_cap);
   // the tables go up from a context-owned pinned buffer (the call returns with the copy still
   // queued): the previous call's upload must have read it before it is refilled
   if (ctx->dc_tab_ev) HIP_TRY(ctx, hipEventSynchronize(ctx->dc_tab_ev));
@@ -643,8 +659,14 @@ int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, d
     L.ntiles = o.ntiles;
     int kp = 2;
     while (kp < o.kmax) kp <<= 1;
-    const size_t sh = (size_t)kp * (sizeof(double) + sizeof(int)) + (size_t)o.kmax * sizeof(double);
-    dc_prep_kernel<<<o.nmerge, DC_SORT_THREADS, sh, st>>>(a, L, kp);
+    if (kp <= DC_LDS_SORT) {
+      const size_t sh = (size_t)kp * (sizeof(double) + sizeof(int));
+      dc_prep_kernel<false><<<o.nmerge, DC_SORT_THREADS, sh, st>>>(a, L, kp, nullptr, nullptr);
+    } else {
+      if ((size_t)o.nmerge * kp > gsort_cap)
+        return set_err(ctx, GPR_E_HIP, "divide and conquer: sort scratch too small");
+      dc_prep_kernel<true><<<o.nmerge, DC_SORT_THREADS, 0, st>>>(a, L, kp, gkey, gidx);
+    }
     LAUNCH_CHECK(ctx);
     dc_rot_kernel<<<dim3((mx + 63) / 64, o.nmerge), 64, 0, st>>>(a, L);
     LAUNCH_CHECK(ctx);

@@ -535,7 +535,8 @@ static int jacobi_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, doub
 // The symmetric eigendecomposition applied to B: by default the tridiagonal reduction
 // (tridiag.hip: A = Q T Q^T, B <- Q^T B inside its launch) followed by divide and conquer on T
 // (dstedc.hip: lam, B <- Z^T B) -- LAPACK syevr's two stages; block Jacobi (above) for n beyond
-// their LDS bounds or when asked for (method 2).  *sweeps: Jacobi sweeps, or the depth of the
+// their bounds (16384), when the reduction's cooperative launch is refused (its workgroups cannot
+// all be resident: another context's persistent work on the device), or when asked for (method 2).  *sweeps: Jacobi sweeps, or the depth of the
 // divide-and-conquer tree.
 int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                   double* dlam, int* sweeps_out, double floor, int method) {
@@ -547,7 +548,12 @@ int sym_eig_apply(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, in
     GPR_TRY(ensure_buf(ctx, &ctx->dtri, &ctx->tri_cap, 2 * (size_t)n + 2));
     double* d = ctx->dtri;
     double* e = d + n + 1;
-    GPR_TRY(sym_tridiag(ctx, dA, n, lda, dB, m, ldb, d, e));
+    const int rc = sym_tridiag(ctx, dA, n, lda, dB, m, ldb, d, e);
+    if (rc == GPR_E_UNSUP) {  // refused before it ran (not co-resident): B untouched -> Jacobi
+      ctx->err.clear();
+      return jacobi_eig_apply(ctx, dA, n, lda, dB, m, ldb, dlam, sweeps_out, floor);
+    }
+    GPR_TRY(rc);
     GPR_TRY(tridiag_eig_apply(ctx, d, e, n, dB, m, ldb, dlam));
     if (sweeps_out) {
       int depth = 0;

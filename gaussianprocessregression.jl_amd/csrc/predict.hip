@@ -1095,7 +1095,12 @@ static int integ_noise_eigen(gpr_ctx* ctx, double* K, const double* k1, double k
                                 ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(dnoise, noise, sizeof(double) * ny, hipMemcpyHostToDevice,
                                 ctx->stream));
-    GPR_TRY(sym_tridiag(ctx, K, n, n, C, ny + 1, n, dd, de));
+    const int rc = sym_tridiag(ctx, K, n, n, C, ny + 1, n, dd, de);
+    if (rc == GPR_E_UNSUP) {  // refused before it ran (not co-resident): K intact, factor per column
+      ctx->err.clear();
+      return 1;
+    }
+    GPR_TRY(rc);
     GPR_TRY(quad_tridiag_solves(ctx, dd, de, n, C, n, ny, dnoise, k2, scr, out));
     std::vector<double> h(2 * (size_t)ny);
     HIP_TRY(ctx, hipMemcpyAsync(h.data(), out, sizeof(double) * 2 * ny, hipMemcpyDeviceToHost,
@@ -1249,7 +1254,7 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   }
   if (qmode != 0) {
     const int rc = integ_noise_eigen(ctx, K, k1, k2, n, dy, ny, ldy, noise, Iout, var, qmode);
-    if (rc != 1) return rc;  // (1: rocSOLVER unavailable or refused the call; K intact)
+    if (rc != 1) return rc;  // (1: the reduction refused (not co-resident) or rocSOLVER unavailable; K intact)
   }
   if (!ctx->quad_seq) {  // the batched launch (GPR_QUAD_SEQ: one column at a time)
     bool declined = false;

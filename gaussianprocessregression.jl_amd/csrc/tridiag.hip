@@ -41,9 +41,11 @@ namespace {
 constexpr int TRD_THREADS = 512;   // 8 waves: one column per wave at a time
 constexpr int TRD_WAVES = TRD_THREADS / 64;
 constexpr int TRD_MAXN = 6144;     // 3 LDS vectors of n doubles per workgroup
+constexpr int TRD_MAXN_G = 16384;  // beyond TRD_MAXN: the vectors in global memory (GV)
 constexpr int TRD_FUSED_M = 1024;  // right-hand sides transformed inside the launch
 
-constexpr int RPT = (TRD_MAXN + TRD_THREADS - 1) / TRD_THREADS;  // rows per thread, one column
+constexpr int RPT = (TRD_MAXN + TRD_THREADS - 1) / TRD_THREADS;      // rows per thread, one column
+constexpr int RPT_G = (TRD_MAXN_G + TRD_THREADS - 1) / TRD_THREADS;  // (the GV variant's)
 
 __device__ __forceinline__ double ld1(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -84,12 +86,12 @@ __device__ long long g_trd_trace[2][TRD_MAXN][6];
 __device__ long long g_trd_wg[TRD_MAXN / 64][256][2];
 #define TRD_WGSTAMP(k)                                                             \
   do {                                                                             \
-    if (tid == 0 && (j & 63) == 0 && w < 256)                                      \
+    if (tid == 0 && (j & 63) == 0 && w < 256 && j < TRD_MAXN)                      \
       g_trd_wg[j >> 6][w][k] = (long long)__builtin_amdgcn_s_memrealtime();        \
   } while (0)
 #define TRD_STAMP(k)                                                                   \
   do {                                                                                 \
-    if (tid == 0 && (w == 0 || w == P - 1))                                            \
+    if (tid == 0 && (w == 0 || w == P - 1) && j < TRD_MAXN)                            \
       g_trd_trace[w == 0 ? 0 : 1][j][k] = (long long)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
@@ -121,6 +123,11 @@ struct TrdArgs {
   double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
   size_t ldb;
   int m;
+  // GV variant (n > TRD_MAXN): step j's vectors in global memory instead of LDS, shared by all
+  // workgroups -- v_j in V's column j (every workgroup writes the same bits there), w_j and
+  // column j + 1 after step j in rings of 4 columns (ld lda): wr[(j & 3) lda], xr[(j & 3) lda]
+  double* wr;
+  double* xr;
 };
 
 // workgroup sum of one value per thread (red: >= TRD_WAVES doubles of LDS), deterministic: the
@@ -139,7 +146,10 @@ __device__ double block_sum(double v, double* red) {
 
 // dlarfg on col[j+1..n-1] in place -> v_j (v_j[j+1] = 1); returns tau_j, *beta = e_j.  Every
 // workgroup computes the same bits (the reflector is formed redundantly everywhere).
-__device__ double trd_reflector(int n, int j, double* col, double* red, double* beta_out) {
+// (src == dst: in place, LDS; the GV variant reads A's column and writes V's, since another
+// workgroup may still be writing the same source values while this one scales them)
+__device__ double trd_reflector(int n, int j, const double* col, double* dst, double* red,
+                                double* beta_out) {
   // (alpha is read before block_sum's barriers: thread 0 overwrites col[j+1] below, and a wave
   // still to read it after that write would form a different reflector)
   const double alpha = col[j + 1];
@@ -152,49 +162,92 @@ __device__ double trd_reflector(int n, int j, double* col, double* red, double* 
     tau = (beta - alpha) / beta;
     scal = 1.0 / (alpha - beta);
   }
-  for (int r = j + 1 + threadIdx.x; r < n; r += TRD_THREADS) col[r] = r == j + 1 ? 1.0 : col[r] * scal;
+  for (int r = j + 1 + threadIdx.x; r < n; r += TRD_THREADS) dst[r] = r == j + 1 ? 1.0 : col[r] * scal;
   __syncthreads();
   *beta_out = beta;
   return tau;
+}
+
+// Poll K handed-off values until none holds the sentinel in the whole workgroup (src[k] ==
+// nullptr: inactive).  Bounded like the LDS variant's loop: false on a time-out here or
+// elsewhere (the caller then ends the workgroup).
+constexpr int TRD_GCH = 4;  // GV exchange: rows per thread per chunk
+template <int K>
+__device__ bool trd_poll(const TrdArgs& a, int n, int j, int* s_ok, double (&v)[K],
+                         const double* const (&src)[K]) {
+  const int tid = threadIdx.x;
+  for (long long spins = 0;; ++spins) {
+    int miss = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) miss |= src[k] != nullptr && trd_unset(v[k]);
+    if (!__syncthreads_or(miss)) return true;
+    if ((spins & 63) == 63) {
+      if (tid == 0) {
+        if (spins > a.spin_limit) st1i(a.err, 1);
+        *s_ok = ld1i(a.err) == 0;
+      }
+      __syncthreads();
+      const bool ok = *s_ok != 0;
+      __syncthreads();
+      if (!ok) return false;
+    }
+    if (n - j > 2048) __builtin_amdgcn_s_sleep(31);
+    else __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (src[k] != nullptr && trd_unset(v[k])) v[k] = ld1(src[k]);
+  }
 }
 
 // Step j's state, identical in every workgroup: vcur = v_j, tau_j; (j > 0) vprev = v_{j-1},
 // wprev = w_{j-1}.  One exchange per step: the pass publishes p_j (and the owner of column
 // j + 1 that column), every workgroup then forms w_j, column j + 1 and v_{j+1} itself.
 // PU: row pairs in flight per lane in the pass (16 from n ~ 800 on: 1-3 % faster at n = 1100-
-// 4096; 8 below, where the extra registers cost more than they hide)
-template <int PU>
+// 4096; 8 below, where the extra registers cost more than they hide).  RP: rows per thread of
+// the exchange (RPT, RPT_G).  GV: the step's vectors in global memory (n > TRD_MAXN, see TrdArgs;
+// every workgroup writes the same bits, and reads a location only after its own write of it has
+// completed -- workgroup barrier -- so what it reads is its own value)
+template <int PU, int RP, bool GV>
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
   extern __shared__ double lds[];
   typedef double d2 __attribute__((ext_vector_type(2)));
   const int n = a.n, P = a.P, w = blockIdx.x, L = a.ldl;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double* red = lds + 3 * (size_t)L;
+  double* red = GV ? lds : lds + 3 * (size_t)L;
   int* s_ok = reinterpret_cast<int*>(red + TRD_WAVES);
   double* s_alpha = red + TRD_WAVES + 1;  // column j+1's entry j+2 after step j (dlarfg's alpha)
   int ivp = 0, iwp = 1, ivc = 2;
   double tj;
 
   {  // v_0 from column 0 (no update before it), redundantly in every workgroup
-    double* c = lds + (size_t)ivc * L;
-    for (int r = tid; r < n; r += TRD_THREADS) c[r] = a.A[r];
-    __syncthreads();
-    const double d0 = c[0];
     double beta;
-    tj = trd_reflector(n, 0, c, red, &beta);
+    double d0;
+    if (GV) {  // column 0 of the work copy is never updated: read it in place, write V's
+      d0 = a.A[0];
+      tj = trd_reflector(n, 0, a.A, a.V, red, &beta);
+    } else {
+      double* c = lds + (size_t)ivc * L;
+      for (int r = tid; r < n; r += TRD_THREADS) c[r] = a.A[r];
+      __syncthreads();
+      d0 = c[0];
+      tj = trd_reflector(n, 0, c, c, red, &beta);
+      if (w == 0)
+        for (int r = 1 + tid; r < n; r += TRD_THREADS) a.V[r] = c[r];
+    }
     if (w == 0 && tid == 0) {
       a.d[0] = d0;
       a.e[0] = beta;
       a.tau[0] = tj;
     }
-    if (w == 0)
-      for (int r = 1 + tid; r < n; r += TRD_THREADS) a.V[r] = c[r];
   }
 
   for (int j = 0; j <= n - 3; ++j) {
-    const double* vprev = lds + (size_t)ivp * L;
-    const double* wprev = lds + (size_t)iwp * L;
-    const double* vcur = lds + (size_t)ivc * L;
+    // (GV, j = 0: v_{-1} and w_{-1} are never used -- the update is skipped -- but the pass
+    // still loads them: point them at v_0, which exists)
+    const double* vprev = GV ? a.V + (size_t)(j > 0 ? j - 1 : 0) * a.lda : lds + (size_t)ivp * L;
+    const double* wprev = GV ? (j > 0 ? a.wr + (size_t)((j - 1) & 3) * a.lda : a.V)
+                             : lds + (size_t)iwp * L;
+    const double* vcur = GV ? a.V + (size_t)j * a.lda : lds + (size_t)ivc * L;
     // ---- the pass over this workgroup's columns c > j, one wave per column: rows from the
     // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), PU row pairs
     // in flight per lane
@@ -269,17 +322,24 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       if (mine < 4) {
         for (int c = w; c < a.m; c += P) {
           double* b = a.B + (size_t)c * a.ldb;
-          double x[RPT];
+          if constexpr (GV) {  // (no register copy of the column: it would spill; read b twice)
+            double dot = 0.0;
+            for (int r = j + 1 + tid; r < n; r += TRD_THREADS) dot += b[r] * vcur[r];
+            const double f = tj * block_sum(dot, red);
+            for (int r = j + 1 + tid; r < n; r += TRD_THREADS) b[r] -= f * vcur[r];
+            continue;
+          }
+          double x[RP];
           double dot = 0.0;
 #pragma unroll
-          for (int k = 0; k < RPT; ++k) {
+          for (int k = 0; k < RP; ++k) {
             const int r = j + 1 + tid + k * TRD_THREADS;
             x[k] = r < n ? b[r] : 0.0;
             dot += r < n ? x[k] * vcur[r] : 0.0;
           }
           const double f = tj * block_sum(dot, red);
 #pragma unroll
-          for (int k = 0; k < RPT; ++k) {
+          for (int k = 0; k < RP; ++k) {
             const int r = j + 1 + tid + k * TRD_THREADS;
             if (r < n) b[r] = x[k] - f * vcur[r];
           }
@@ -306,63 +366,104 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     // these addresses is written once per launch and holds the sentinel until then, so each
     // value is its own arrival flag: all loads are issued at once, and only values still
     // holding the sentinel are loaded again (sc1), until none is left in the workgroup.
-    double* wnew = lds + (size_t)ivp * L;  // (v_{j-1}'s slot)
-    double* cnew = lds + (size_t)iwp * L;  // (w_{j-1}'s slot) -> v_{j+1}
+    double* wnew = GV ? a.wr + (size_t)(j & 3) * a.lda : lds + (size_t)ivp * L;  // (v_{j-1}'s slot)
+    double* cnew = GV ? a.xr + (size_t)(j & 3) * a.lda : lds + (size_t)iwp * L;  // (w_{j-1}'s) -> v_{j+1}
+    // v_{j+1}'s destination: in place in LDS; V's column j + 1 for GV (not in place: a slower
+    // workgroup may still be writing column j + 1's values into the ring slot)
+    double* vnext = GV ? a.V + (size_t)(j + 1) * a.lda : cnew;
     const double* pj = a.pbuf + (size_t)j * a.lda;
     const double* cp = a.cpub + (size_t)(j + 1) * a.lda;
     const double* pp = a.parts + (size_t)j * P;
-    double pr[RPT], cr[RPT];
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r = j + 1 + tid + k * TRD_THREADS;
-      pr[k] = r < n ? ld1(&pj[r]) : 0.0;
-      cr[k] = r < n ? ld1(&cp[r]) : 0.0;
-    }
-    double pc = ld1(&pj[j + 1]);
-    double pq = tid < P ? ld1(&pp[tid]) : 0.0;
-    for (long long spins = 0;; ++spins) {
-      int miss = trd_unset(pc) | trd_unset(pq);
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) miss |= trd_unset(pr[k]) | trd_unset(cr[k]);
-      if (!__syncthreads_or(miss)) break;
-      if ((spins & 63) == 63) {  // bounded: a time-out here or elsewhere ends every workgroup
-        if (tid == 0) {
-          if (spins > a.spin_limit) st1i(a.err, 1);
-          *s_ok = ld1i(a.err) == 0;
-        }
-        __syncthreads();
-        const bool ok = *s_ok != 0;
-        __syncthreads();
-        if (!ok) return;
-      }
-      // long steps (workgroups arrive microseconds apart): poll less often, so the early
-      // arrivals' re-loads leave the memory system to the passes still streaming
-      if (n - j > 2048) __builtin_amdgcn_s_sleep(31);
-      else __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const int r = j + 1 + tid + k * TRD_THREADS;
-        if (trd_unset(pr[k])) pr[k] = ld1(&pj[r]);
-        if (trd_unset(cr[k])) cr[k] = ld1(&cp[r]);
-      }
-      if (trd_unset(pc)) pc = ld1(&pj[j + 1]);
-      if (trd_unset(pq)) pq = ld1(&pp[tid]);
-    }
-    TRD_STAMP(3);
-    const double kj = 0.5 * tj * block_sum(pq, red);
-    TRD_STAMP(4);
-    const double wc = pc - kj * vcur[j + 1], vc = vcur[j + 1];
     double xn = 0.0;
+    if constexpr (!GV) {
+      double pr[RP], cr[RP];
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r = j + 1 + tid + k * TRD_THREADS;
-      if (r < n) {
-        const double wr = pr[k] - kj * vcur[r];
-        const double x = cr[k] - (vcur[r] * wc + wr * vc);
-        wnew[r] = wr;
-        cnew[r] = x;
-        if (r >= j + 3) xn += x * x;
-        if (r == j + 2) *s_alpha = x;
+      for (int k = 0; k < RP; ++k) {
+        const int r = j + 1 + tid + k * TRD_THREADS;
+        pr[k] = r < n ? ld1(&pj[r]) : 0.0;
+        cr[k] = r < n ? ld1(&cp[r]) : 0.0;
+      }
+      double pc = ld1(&pj[j + 1]);
+      double pq = tid < P ? ld1(&pp[tid]) : 0.0;
+      for (long long spins = 0;; ++spins) {
+        int miss = trd_unset(pc) | trd_unset(pq);
+#pragma unroll
+        for (int k = 0; k < RP; ++k) miss |= trd_unset(pr[k]) | trd_unset(cr[k]);
+        if (!__syncthreads_or(miss)) break;
+        if ((spins & 63) == 63) {  // bounded: a time-out here or elsewhere ends every workgroup
+          if (tid == 0) {
+            if (spins > a.spin_limit) st1i(a.err, 1);
+            *s_ok = ld1i(a.err) == 0;
+          }
+          __syncthreads();
+          const bool ok = *s_ok != 0;
+          __syncthreads();
+          if (!ok) return;
+        }
+        // long steps (workgroups arrive microseconds apart): poll less often, so the early
+        // arrivals' re-loads leave the memory system to the passes still streaming
+        if (n - j > 2048) __builtin_amdgcn_s_sleep(31);
+        else __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < RP; ++k) {
+          const int r = j + 1 + tid + k * TRD_THREADS;
+          if (trd_unset(pr[k])) pr[k] = ld1(&pj[r]);
+          if (trd_unset(cr[k])) cr[k] = ld1(&cp[r]);
+        }
+        if (trd_unset(pc)) pc = ld1(&pj[j + 1]);
+        if (trd_unset(pq)) pq = ld1(&pp[tid]);
+      }
+      TRD_STAMP(3);
+      const double kj = 0.5 * tj * block_sum(pq, red);
+      TRD_STAMP(4);
+      const double wc = pc - kj * vcur[j + 1], vc = vcur[j + 1];
+#pragma unroll
+      for (int k = 0; k < RP; ++k) {
+        const int r = j + 1 + tid + k * TRD_THREADS;
+        if (r < n) {
+          const double wr = pr[k] - kj * vcur[r];
+          const double x = cr[k] - (vcur[r] * wc + wr * vc);
+          wnew[r] = wr;
+          cnew[r] = x;
+          if (r >= j + 3) xn += x * x;
+          if (r == j + 2) *s_alpha = x;
+        }
+      }
+    } else {
+      // GV (n > TRD_MAXN): the same exchange in chunks of TRD_GCH rows per thread (all of a
+      // column's rows in registers at once would spill): the partial sums and p_j[j + 1] first
+      // (w_j needs their sum), then each chunk of p_j and column j + 1 polled and consumed
+      double pv[2] = {ld1(&pj[j + 1]), tid < P ? ld1(&pp[tid]) : 0.0};
+      const double* ps[2] = {&pj[j + 1], tid < P ? &pp[tid] : nullptr};
+      if (!trd_poll<2>(a, n, j, s_ok, pv, ps)) return;
+      TRD_STAMP(3);
+      const double kj = 0.5 * tj * block_sum(pv[1], red);
+      TRD_STAMP(4);
+      const double wc = pv[0] - kj * vcur[j + 1], vc = vcur[j + 1];
+      for (int k0 = 0; j + 1 + k0 * TRD_THREADS < n; k0 += TRD_GCH) {  // (uniform bound)
+        double xv[2 * TRD_GCH];
+        const double* xs[2 * TRD_GCH];
+#pragma unroll
+        for (int k = 0; k < TRD_GCH; ++k) {
+          const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
+          xs[2 * k] = r < n ? &pj[r] : nullptr;
+          xs[2 * k + 1] = r < n ? &cp[r] : nullptr;
+          xv[2 * k] = r < n ? ld1(&pj[r]) : 0.0;
+          xv[2 * k + 1] = r < n ? ld1(&cp[r]) : 0.0;
+        }
+        if (!trd_poll<2 * TRD_GCH>(a, n, j, s_ok, xv, xs)) return;
+#pragma unroll
+        for (int k = 0; k < TRD_GCH; ++k) {
+          const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
+          if (r < n) {
+            const double wr = xv[2 * k] - kj * vcur[r];
+            const double x = xv[2 * k + 1] - (vcur[r] * wc + wr * vc);
+            wnew[r] = wr;
+            cnew[r] = x;
+            if (r >= j + 3) xn += x * x;
+            if (r == j + 2) *s_alpha = x;
+          }
+        }
       }
     }
     const double xnorm2 = block_sum(xn, red);  // (its barriers publish cnew / wnew)
@@ -382,8 +483,8 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       double* vj = a.V + (size_t)(j + 1) * a.lda;
       for (int r = j + 2 + tid; r < n; r += TRD_THREADS) {
         const double v = r == j + 2 ? 1.0 : cnew[r] * scal;
-        cnew[r] = v;
-        if (out) vj[r] = v;
+        vnext[r] = v;
+        if (out && !GV) vj[r] = v;
       }
       if (out && tid == 0) {
         a.e[j + 1] = beta;
@@ -610,12 +711,36 @@ __global__ void trd_copy_kernel(const double* __restrict__ A, size_t lda, int n,
 
 }  // namespace
 
+namespace {
+// the work copy and the exchange buffers (4 n^2 doubles) are not kept past the call once they
+// pass 1 GB (n > ~5.8k; re-allocating costs far less than the reduction itself)
+int release_eig_scratch(gpr_ctx* ctx) {
+  if (ctx->deig && ctx->eig_cap * sizeof(double) > (size_t)(1ull << 30)) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(ctx->deig));
+    ctx->deig = nullptr;
+    ctx->eig_cap = 0;
+  }
+  return 0;
+}
+
+template <int PU, int RP, bool GV>
+const void* trd_kernel_ptr() {
+  return reinterpret_cast<const void*>(&sytrd_kernel<PU, RP, GV>);
+}
+}  // namespace
+
 // A (n x n, lda; symmetric, both triangles read) = Q T Q^T: d[n], e[n-1] (device) and, when
-// m > 0, B <- Q^T B (n x m, ldb).  Workspace in ctx->deig.  n <= TRD_MAXN.
+// m > 0, B <- Q^T B (n x m, ldb).  Workspace in ctx->deig.  n <= TRD_MAXN_G.
+// Returns GPR_E_UNSUP -- before touching B -- when n is beyond the bound or the launch's
+// workgroups cannot all be resident at once (the exchange needs every one of them every step:
+// the launch is cooperative, so the runtime refuses it up front rather than letting resident
+// workgroups spin on absent ones); the callers then take another route.
 int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                 double* dd, double* de) {
   if (n <= 0) return 0;
-  if (n > TRD_MAXN) return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: n = %d > %d", n, TRD_MAXN);
+  if (n > TRD_MAXN_G) return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: n = %d > %d", n, TRD_MAXN_G);
+  const bool gv = n > TRD_MAXN;
   hipStream_t st = ctx->stream;
   if (ctx->ncu <= 0) {
     hipDeviceProp_t prop;
@@ -633,6 +758,18 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 #ifdef GPR_TESTING
   if (const char* e = getenv("GPR_TRD_COLS")) cols = std::max(1, atoi(e));  // (tuning sweeps)
 #endif
+  const size_t shmem = ((gv ? 0 : 3 * (size_t)((n + 1) & ~1)) + TRD_WAVES + 2) * sizeof(double);
+  const void* kfn = gv ? trd_kernel_ptr<16, RPT_G, true>()
+                       : n >= 800 ? trd_kernel_ptr<16, RPT, false>() : trd_kernel_ptr<8, RPT, false>();
+  // co-residency: one workgroup per CU (the launch bound and, for the LDS variant, its vectors
+  // allow no more); none at all is refused here, and the cooperative launch below refuses a grid
+  // that cannot be resident as a whole
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, TRD_THREADS, shmem) != hipSuccess ||
+      per_cu <= 0) {
+    (void)hipGetLastError();
+    return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: no resident workgroup possible");
+  }
   const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
   // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), tau, dlast, then ints
   const size_t nW = ld * n;
@@ -649,7 +786,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
                         ? 2 * (size_t)n2 * QB + 2 * (size_t)QB * QB + 2 * (size_t)QB * m +
                               (size_t)gw_S * QB * (QB + m)
                         : 0;
-  const size_t need = 4 * nW + (size_t)n * P + (size_t)n + 8 + nI + nQ;
+  const size_t nG = gv ? 8 * ld : 0;  // (GV: the w and column-(j+1) rings, 4 columns each)
+  const size_t need = 4 * nW + (size_t)n * P + (size_t)n + 8 + nI + nQ + nG;
   GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
   double* W = ctx->deig;
   double* V = W + nW;
@@ -661,6 +799,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   int* ints = reinterpret_cast<int*>(dlast + 8);
   int* err = ints + n;
   double* Vb = reinterpret_cast<double*>(ints) + nI;  // the Q^T B blocks'
+  double* rings = Vb + nQ;
   TimerScope ts(ctx, TC_OTHER, 4.0 * n * (double)n * n / 3.0);
   if (n == 1 || n == 2) {  // already tridiagonal: T = A, Q = I
     HIP_TRY(ctx, hipMemcpy2DAsync(dd, sizeof(double), dA, sizeof(double) * (lda + 1),
@@ -701,17 +840,22 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;
   a.m = fused_b ? m : 0;
-  const size_t shmem = (3 * (size_t)a.ldl + TRD_WAVES + 2) * sizeof(double);
-  if (n >= 800)
-    sytrd_kernel<16><<<P, TRD_THREADS, shmem, st>>>(a);
-  else
-    sytrd_kernel<8><<<P, TRD_THREADS, shmem, st>>>(a);
-  LAUNCH_CHECK(ctx);
+  a.wr = gv ? rings : nullptr;
+  a.xr = gv ? rings + 4 * ld : nullptr;
+  // cooperative: all P workgroups resident together, or the runtime refuses the launch (nothing
+  // has run then: B is untouched, and the caller falls back)
+  void* kargs[] = {&a};
+  if (hipLaunchCooperativeKernel(kfn, dim3(P), dim3(TRD_THREADS), kargs, (unsigned)shmem, st) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: cooperative launch of %d workgroups "
+                   "refused", P);
+  }
   int herr = 0;
   HIP_TRY(ctx, hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, st));
   HIP_TRY(ctx, hipStreamSynchronize(st));
   if (herr) return set_err(ctx, GPR_E_HIP, "tridiagonal reduction: a wait timed out");
-  if (m <= 0 || fused_b) return 0;
+  if (m <= 0 || fused_b) return release_eig_scratch(ctx);
   // B <- Q^T B = H_{n-3} ... H_0 B, 64 reflectors per block: B -= V_b (T_b^T (V_b^T B))
   const int nref_all = n - 2;
   double* VbT = Vb + (size_t)n2 * QB;
@@ -750,7 +894,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
     u.alpha = -1.0; u.beta = 1.0;
     GPR_TRY(launch_gemm_tn(ctx, u, TC_OTHER));
   }
-  return 0;
+  return release_eig_scratch(ctx);
 }
 
 // out[2j] = Iout_j, out[2j+1] = var_j for the quadrature (see quad_tridiag_kernel); C = Q^T [Y | k1]
@@ -776,7 +920,7 @@ int quad_tridiag_solves(gpr_ctx* ctx, const double* dd, const double* de, int n,
   return 0;
 }
 
-bool sym_tridiag_ok(int n) { return n >= 1 && n <= TRD_MAXN; }
+bool sym_tridiag_ok(int n) { return n >= 1 && n <= TRD_MAXN_G; }
 
 #ifdef GPR_TESTING
 // the last reduction's phase stamps (100 MHz clock): [2][n][6] long longs

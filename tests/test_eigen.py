@@ -272,14 +272,16 @@ def test_sytrd_handoff_timeout_drains_and_context_recovers():
     run_fault_scenario("trd_timeout")
 
 
-def test_syev_largest_size_known_spectrum():
-    """n = 6144, the reduction's and the divide and conquer's largest size (three n-vectors of
-    LDS per workgroup; the merge sort's LDS): A = H3 H2 H1 diag(ev) H1 H2 H3 with Householder
-    H_k, so the eigenvalues are ev exactly; eigenvalues within 4 n eps ||A||, column norms of
-    P^T B preserved, and the quadratic form B^T (A + s I)^{-1} B from the eigenpairs against the
-    same form from the known factors.  One past the bound, the reduction reports GPR_E_UNSUP."""
-    n = 6144
-    rng = np.random.default_rng(6144)
+@pytest.mark.parametrize("n", [6144, 8192, 8200])
+def test_syev_large_known_spectrum(n):
+    """Large sizes with a known spectrum: n = 6144, the LDS variants' largest (three n-vectors
+    of LDS per reduction workgroup; the merge sort in LDS); 8192, the reduction's global-vector
+    variant (its vectors beyond LDS) with the top merge still sorted in LDS; 8200, the top merge
+    sorted in global memory.  A = H3 H2 H1 diag(ev) H1 H2 H3 with Householder H_k, so the
+    eigenvalues are ev exactly; eigenvalues within 4 n eps ||A||, column norms of P^T B
+    preserved, and the quadratic form B^T (A + s I)^{-1} B from the eigenpairs against the same
+    form from the known factors."""
+    rng = np.random.default_rng(n)
     ev = np.sort(rng.standard_normal(n)) * 3.0
     ev[::97] = ev[0]  # a few exact repeats: deflation on the top merges
     ev = np.sort(ev)
@@ -307,10 +309,68 @@ def test_syev_largest_size_known_spectrum():
     got = C.T @ (C / (lam + s)[:, None])
     cond = np.abs(ev + s).max() / np.abs(ev + s).min()
     np.testing.assert_allclose(got, want, rtol=1e-10 * cond, atol=1e-10 * cond * np.abs(want).max())
-    dA = ctx.colmajor(np.eye(n + 1))
-    dd, de = ctx.empty(n + 1), ctx.empty(n)
+
+
+def test_sytrd_and_syev_beyond_bound():
+    """One past the reduction's bound (n = 16385) the reduction reports GPR_E_UNSUP before it
+    reads A (a 1-element buffer suffices); the eigendecomposition takes block Jacobi there."""
+    ctx = G.Context(0)
+    n = 16385
+    dA, dd, de = ctx.empty(1), ctx.empty(1), ctx.empty(1)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n + 1, n + 1, None, 0, n + 1, P(dd), P(de)) == -4
+    assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, n, None, 0, n, P(dd), P(de)) == -4
+
+
+def test_sytrd_se_kernel_quadratic_form_global_vectors():
+    """The quadrature's quantity at n = 8192 (the reduction's global-vector variant) on the
+    reference's SE + WN kernel, d = 8: B^T (K + s I)^{-1} B = (Q^T B)^T (T + s I)^{-1} (Q^T B)
+    for a positive shift, a negative one keeping K + s I definite (lambda_min >= sigma_n^2) and
+    one below -lambda_max (negative definite); the condition number from the bounds
+    sigma_n^2 <= lambda <= ||K||_1 (no O(n^3) eigensolve on the host)."""
+    import scipy.linalg as sla
+    n, dim = 8192, 8
+    rng = np.random.default_rng(8192)
+    x = rng.random((dim, n))
+    kinds = [O.SE, O.WN]
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    K = O.kernel(kinds, hp, x)
+    B = np.c_[rng.random((n, 2)), O.antideriv_se(x, hp, np.zeros(dim), np.ones(dim))]
+    ctx = G.Context(0)
+    d, e, C = _sytrd(ctx, K, B)
+    np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-12)
+    lmax = np.abs(K).sum(0).max()
+    lmin = hp[-1] ** 2
+    for s in (1e-3, -0.5 * lmin, -1.5 * lmax):
+        want = B.T @ np.linalg.solve(K + s * np.eye(n), B)
+        got = C.T @ sla.solve_banded((1, 1), np.vstack([np.r_[0.0, e], d + s, np.r_[e, 0.0]]), C)
+        lo = lmin + s if s > -lmin else abs(s) - lmax
+        cond = (lmax + abs(s)) / lo
+        np.testing.assert_allclose(got, want, rtol=1e-10 * cond,
+                                   atol=1e-10 * cond * np.abs(want).max())
+
+
+def test_sytrd_cooperative_beside_concurrent_kernel():
+    """The reduction's launch is cooperative (every workgroup resident, or refused up front):
+    with a long matrix product running on another stream of the same device the reduction
+    still completes and gives the same d, e and Q^T B as alone (the caller would fall back,
+    not spin, if the runtime could not make every workgroup resident)."""
+    import torch
+    n = 2048
+    rng = np.random.default_rng(77)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    B = rng.standard_normal((n, 3))
+    ctx = G.Context(0)
+    d0, e0, C0 = _sytrd(ctx, A, B)
+    side = torch.cuda.Stream()
+    M = torch.randn(6144, 6144, dtype=torch.float64, device="cuda")
+    with torch.cuda.stream(side):
+        for _ in range(6):
+            M = (M @ M) * 1e-3
+    d, e, C = _sytrd(ctx, A, B)
+    side.synchronize()
+    assert torch.isfinite(M).all()
+    assert np.array_equal(d, d0) and np.array_equal(e, e0) and np.array_equal(C, C0)
 
 
 @pytest.mark.parametrize("n,m", [(300, 4), (700, 1100)])

@@ -202,6 +202,38 @@ def test_integrate_sample_noise_negative(knobs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("quad", ["auto", "1"])
+def test_integrate_sample_noise_negative_large(quad, knobs):
+    """n = 8192 (beyond the LDS-bound reduction of round 5): a positive shift, a negative one
+    that keeps K + s I positive definite (lambda_min(K) >= sigma_n^2) and one below -lambda_max
+    (negative definite, as the reference's eigen path allows).  The default tries the per-column
+    factorisations (3 columns), meets the indefinite shift and hands the call to the tridiagonal
+    reduction (its global-vector variant) -- no PosDefException and no block Jacobi; knob 1 takes
+    the reduction directly.  Expected values by a dense LU solve of K + s I (the same function
+    k1' (K + s I)^{-1} y the reference's eigen path evaluates)."""
+    if quad != "auto":
+        knobs("GPR_QUAD_EIGEN", int(quad))
+    dim, n = 4, 8192
+    kinds = [O.SE, O.WN]
+    rng = np.random.default_rng(8192)
+    x = rng.random((dim, n))
+    Y = rng.random((n, 3))
+    hp = O.default_hp(kinds, dim, length=2.0, noise=0.05)
+    md = G.GPRModel(G.SquaredExp() + G.WhiteNoise(), hp, x, Y)
+    a, b = np.zeros(dim), np.ones(dim)
+    K = O.kernel(kinds, hp, x)
+    lmax = np.abs(K).sum(0).max()
+    noise = np.array([1e-3, -0.5 * hp[-1] ** 2, -1.5 * lmax])
+    I, v = G.integrate(md, a, b, sample_noise=noise)
+    k1 = O.antideriv_se(x, hp, a, b)
+    k2 = O.antideriv2_se(hp, a, b)
+    for j, s in enumerate(noise):
+        sol = np.linalg.solve(K + s * np.eye(n), np.c_[Y[:, j], k1])
+        np.testing.assert_allclose(I[j], k1 @ sol[:, 0], rtol=1e-7)
+        np.testing.assert_allclose(v[j], k2 - k1 @ sol[:, 1], rtol=1e-6, atol=1e-10 * k2)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dim,n,k", [(1, 100, 100), (2, 200, 300), (4, 300, 200)])
 def test_integrate_zero_noise_reference(dim, n, k):
     """test/test_integrate.jl:113-126 (random hp as GPRModel(SquaredExp(), x, y))."""

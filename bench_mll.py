@@ -43,44 +43,52 @@ def parse():
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--d", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-n", type=int, default=4096,
-                    help="bounded CPU sample: the oracle's C4 evaluation at this N, each stage "
+    ap.add_argument("--cpu-n", type=int, default=8192,
+                    help="bounded CPU sample: the C4 evaluation at this N, each stage "
                          "extrapolated to --n by its complexity")
     return ap.parse_args()
 
 
 def cpu_baseline(a, hp):
-    """The CPU oracle (test infrastructure; this leg only) on a bounded sample of the C4
-    evaluation: loss_grad! for an MllGradCache in the reference's order (src/cost.jl:83-126 --
-    K, cholesky!, ldiv!, K^{-1} = ldiv!(kchol, I), the MLL and every dK/dtheta_i's
-    grad(MLL, ...) term, LogScale) at N = a.cpu_n, d = a.d, one run after a warm-up, each
-    stage scaled to N = a.n by its complexity (N^2, N^3, N^2, N^3, N^2).  Threads: the box's CPU
-    share (OMP_NUM_THREADS) for OpenBLAS, reported by threadpoolctl."""
-    import scipy.linalg as sla
+    """The CPU restatement of the reference's C4 evaluation (test infrastructure; this leg
+    only): loss_grad! for an MllGradCache in the reference's order and with its algorithms
+    (src/cost.jl:96-126) -- the per-part matrices K_p and K = sum K_p + sigma_n^2 I (kernels!,
+    threaded C), cholesky! (LAPACK dpotrf), alpha = ldiv!(kchol, y) (dpotrs), K^{-1} =
+    ldiv!(kchol, I) (dpotrs with N right-hand sides: 2 N^3, as written), the MLL and the
+    gradient loop of oracle/mll_grad_cpu.c (per component: materialise dK_i, dgemv, Frobenius
+    dot -- the reference's memory traffic).  Run at N = a.cpu_n (default 8192, the whole
+    evaluation), median of 3 after a warm-up; stages scaled to N = a.n by their complexity
+    (N^2, N^3, N^2, N^3, N^2).  Threads: the box's CPU share (OMP_NUM_THREADS) for OpenMP and
+    OpenBLAS, reported by threadpoolctl."""
+    import scipy.linalg.lapack as lap
     from threadpoolctl import threadpool_info, threadpool_limits
 
     sys.path.insert(0, ROOT)
     from oracle import gpr_oracle as O
+    from oracle.cpu_kbuild import mll_grad_cpu, part_kernels_cpu
 
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     n, d = a.cpu_n, a.d
     kinds = [O.SE, O.WN]
     x = np.random.default_rng(0).random((d, n))
     y = np.sin(x.sum(0)) ** 2
+    eye = np.asfortranarray(np.eye(n))
 
-    def run(x, y):
+    def run():
         t = [time.perf_counter()]
-        K = O.kernel(kinds, hp, x)
+        Kp = part_kernels_cpu(kinds, hp, x)          # kernels!(kerns, ...) (one SE part)
+        K = np.asfortranarray(Kp.sum(0).T)           # kchol_base .= sum(kerns)
+        K[np.diag_indices(n)] += hp[-1] ** 2         # add_noise!
         t.append(time.perf_counter())
-        U = sla.cholesky(K, lower=False, check_finite=False)
+        U, info = lap.dpotrf(K, lower=0, clean=0, overwrite_a=1)
+        assert info == 0, info
         t.append(time.perf_counter())
-        alpha = O.cho_solve_upper(U, y)
+        alpha, info = lap.dpotrs(U, y, lower=0)
         t.append(time.perf_counter())
-        Kinv = O.kinv_from_upper(U)
+        Kinv, info = lap.dpotrs(U, eye, lower=0)     # ldiv!(kchol, K^-1 = I)
         t.append(time.perf_counter())
-        g = np.array([O.mll_grad_term(O.kernel_grad(kinds, i, hp, x), alpha, Kinv)
-                      for i in range(1, len(hp) + 1)]) * hp
         val = O.mll_value(U, y, alpha)
+        g = mll_grad_cpu(kinds, hp, x, alpha, Kinv, Kp=Kp) * hp  # LogScale: G .*= hp
         t.append(time.perf_counter())
         assert np.isfinite(g).all() and np.isfinite(val)
         return np.diff(t)
@@ -90,20 +98,25 @@ def cpu_baseline(a, hp):
                  "threads": i.get("num_threads")}
                 for i in threadpool_info() if i.get("user_api") == "blas"
                 and "scipy.libs" in i.get("filepath", "")]
-        run(x[:, :256], y[:256])  # (warm-up: libraries and code paths, on 256 points)
-        t = run(x, y)  # one timed run: its 18 dK/dtheta terms alone take ~20 s at N = 4096
+        run()  # warm-up
+        t = np.median(np.stack([run() for _ in range(3)]), axis=0)
     r = a.n / n
     scale = np.array([r ** 2, r ** 3, r ** 2, r ** 3, r ** 2])
     t_eval = float(np.sum(t * scale))
+    D = len(hp)
     return {
         "value": 1.0 / t_eval, "unit": "loss_grad! evaluations/s", "cores": threads,
         "kind": "port", "blas": blas,
-        "measured_config": {"N": n, "d": d, "stage_s": [round(v, 4) for v in t.tolist()]},
-        "sample": (f"oracle (NumPy/SciPy OpenBLAS, {threads} threads) C4 evaluation at N={n}, "
-                   f"d={d} (one run after a 256-point warm-up): stages [kernel, dpotrf, dpotrs, "
-                   f"K^-1, mll+{len(hp)} grad terms] = {[round(v, 4) for v in t.tolist()]} s; "
-                   f"extrapolated to N={a.n} by N^2 / N^3 / N^2 / N^3 / N^2 -> {t_eval:.2f} s "
-                   f"per evaluation"),
+        "measured_config": {"N": n, "d": d, "D": D, "stage_s": [round(v, 4) for v in t.tolist()]},
+        "sample": (f"C restatement of the reference's evaluation ({threads} threads: OpenMP "
+                   f"K_p build and gradient loop -- dK_i materialised, dgemv, Frobenius dot per "
+                   f"component -- and OpenBLAS dpotrf / dpotrs / dpotrs(U, I)) at N={n}, d={d}, "
+                   f"D={D} (median of 3 after 1 warm-up): stages [kernels, dpotrf, dpotrs, "
+                   f"K^-1 = dpotrs(U, I), mll + {D} grad terms] = "
+                   f"{[round(v, 4) for v in t.tolist()]} s"
+                   + ("" if n == a.n else
+                      f"; extrapolated to N={a.n} by N^2 / N^3 / N^2 / N^3 / N^2")
+                   + f" -> {t_eval:.2f} s per evaluation"),
     }
 
 

@@ -22,6 +22,10 @@ def _load():
         _lib.kbuild_cpu.argtypes = [ctypes.c_int, ctypes.c_int, D, ctypes.c_int, D, ctypes.c_int,
                                     D, D, ctypes.c_int, ctypes.c_double, ctypes.c_double, D]
         _lib.kbuild_cpu.restype = None
+        I = ctypes.POINTER(ctypes.c_int)
+        _lib.mll_grad_cpu.argtypes = [ctypes.c_int, ctypes.c_int, D, ctypes.c_int, I, D, D, D,
+                                      ctypes.c_double, D, D, D, D, D]
+        _lib.mll_grad_cpu.restype = None
     return _lib
 
 
@@ -43,6 +47,47 @@ def kbuild_cpu(kinds, hp, x, xp=None, eps=O.EPS_DEFAULT) -> np.ndarray:
                    1 if (wn and xp is None) else 0, float(wn[0][0] ** 2) if wn else 0.0, eps,
                    P(K))
     return K.T
+
+
+def part_kernels_cpu(kinds, hp, x, eps=O.EPS_DEFAULT):
+    """kernels!(kerns, covar, hp, x) (src/compose_covar.jl:80-107): one n x n matrix per SE
+    part (eps on its diagonal), stacked (nse, n, n) -- each column-major n x n."""
+    d = x.shape[0]
+    hps = O.split_hp(kinds, np.asarray(hp, dtype=np.float64), d)
+    se = [h for k, h in zip(kinds, hps) if k == O.SE]
+    out = np.empty((len(se), x.shape[1], x.shape[1]))
+    for p, h in enumerate(se):
+        out[p] = kbuild_cpu([O.SE], h, x, None, eps).T  # (transpose of a symmetric matrix)
+    return out
+
+
+def mll_grad_cpu(kinds, hp, x, alpha, Kinv, Kp=None, eps=O.EPS_DEFAULT) -> np.ndarray:
+    """grad!(dL, MLL, md, tc) (src/cost.jl:119-126) by the threaded C restatement of the
+    reference's per-component loop (oracle/mll_grad_cpu.c: materialise dK_i, dgemv, Frobenius
+    dot, for each of the D components).  Kp: the per-part matrices (part_kernels_cpu), built
+    here if not given.  Same values as O.mll_grad's loop (tests/test_oracle.py)."""
+    lib = _load()
+    d, n = x.shape
+    hp = np.asarray(hp, dtype=np.float64)
+    hps = O.split_hp(kinds, hp, d)
+    se = [h for k, h in zip(kinds, hps) if k == O.SE]
+    wn = [h for k, h in zip(kinds, hps) if k == O.WN]
+    if Kp is None:
+        Kp = part_kernels_cpu(kinds, hp, x, eps)
+    Kp = np.ascontiguousarray(Kp)
+    sig = np.array([h[0] for h in se], dtype=np.float64)
+    ls = np.ascontiguousarray(np.stack([h[1:] for h in se]), dtype=np.float64)
+    pk = (ctypes.c_int * len(kinds))(*[1 if k == O.SE else 2 for k in kinds])
+    xc = np.ascontiguousarray(x.T)
+    al = np.ascontiguousarray(alpha, dtype=np.float64)
+    Ki = np.asfortranarray(Kinv)
+    dK = np.empty((n, n))
+    tt = np.empty(n)
+    g = np.empty(len(hp))
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    lib.mll_grad_cpu(d, n, P(xc), len(kinds), pk, P(Kp), P(sig), P(ls),
+                     float(wn[0][0]) if wn else 0.0, P(al), P(Ki), P(dK), P(tt), P(g))
+    return g
 
 
 def fit_upper_inplace(kinds, hp, x, y, eps=O.EPS_DEFAULT, backend="scipy"):

@@ -64,7 +64,23 @@ struct DcArgs {
   int* K;          // per merge
   int* nrot;
   double* rho2;    // per merge: 2 |beta|
+  int delay;       // (test build) GPR_DC_DELAY: late-wave injection, see DC_DELAY
 };
+
+// Late-wave injection (test build only, GPR_DC_DELAY = d > 0): one wave in three (rotating with
+// the site and the workgroup) sleeps d x ~8k cycles before reads that follow other waves' LDS or
+// global writes, so a missing barrier shows as a wrong result (as tridiag.hip's TRD_DELAY).
+#ifdef GPR_TESTING
+#define DC_DELAY(site)                                                                  \
+  do {                                                                                  \
+    if (a.delay > 0 && ((int)blockIdx.x + (int)(threadIdx.x >> 6) + (site)) % 3 == 0)   \
+      for (int q_ = 0; q_ < a.delay; ++q_) __builtin_amdgcn_s_sleep(127);              \
+  } while (0)
+#else
+#define DC_DELAY(site) \
+  do {                 \
+  } while (0)
+#endif
 
 __device__ __forceinline__ double dwave_sum(double v) {
 #pragma unroll
@@ -156,6 +172,7 @@ __global__ __launch_bounds__(DC_SORT_THREADS) void dc_prep_kernel(DcArgs a, DcLe
   for (int size = 2; size <= kp; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       __syncthreads();
+      DC_DELAY(size + stride);  // (a late wave of the previous stage's exchanges)
       for (int i = tid; i < kp / 2; i += DC_SORT_THREADS) {
         const int lo_i = 2 * i - (i & (stride - 1));
         const int hi_i = lo_i + stride;
@@ -170,6 +187,7 @@ __global__ __launch_bounds__(DC_SORT_THREADS) void dc_prep_kernel(DcArgs a, DcLe
         }
       }
     }
+  DC_DELAY(1);
   __syncthreads();
   if (tid == 0) {
     double dm = 0.0, zm = 0.0;
@@ -460,6 +478,7 @@ __global__ __launch_bounds__(256) void dc_apply_kernel(DcArgs a, DcLevel L) {
         Us[ii][q] = (i < K && jj < jend) ? zh[i] / dc_delta(dl, org, tau, i, jj) * a.nrm[lo + jj] : 0.0;
         Xs[ii][q] = (i < K && cc < a.mx) ? a.X[(size_t)a.nd_row[lo + i] + (size_t)cc * a.ldx] : 0.0;
       }
+      DC_DELAY(i0);  // (a late writer of the staged U / X chunk)
       __syncthreads();
 #pragma unroll 4
       for (int ii = 0; ii < 16; ++ii) {
@@ -643,6 +662,9 @@ int tridiag_eig_apply(gpr_ctx* ctx, const double* dd, const double* de, int n, d
                                 hipMemcpyHostToDevice, st));
     HIP_TRY(ctx, hipEventRecord(ctx->dc_tab_ev, st));
   }
+#ifdef GPR_TESTING
+  a.delay = getenv("GPR_DC_DELAY") ? std::max(0, atoi(getenv("GPR_DC_DELAY"))) : 0;
+#endif
   TimerScope ts(ctx, TC_OTHER, 0.0);
   dc_init_kernel<<<512, 256, 0, st>>>(dd, de, n, dC, (size_t)ldc, m, X, ldx, dlam);
   LAUNCH_CHECK(ctx);

@@ -79,6 +79,24 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Late-wave injection (test build only, GPR_TRD_DELAY = d > 0): at each site, one wave in three
+// (rotating with the site, the step and the workgroup) sleeps d x ~8k cycles.  Placed before the
+// reads that follow a single-thread / single-wave LDS write and before each hand-off poll, it
+// forces the schedules in which a reader is late (or a writer is), so a missing barrier or
+// flag shows as a wrong result instead of depending on timing.  (It exposes the round-5 dlarfg
+// alpha race deterministically: waves reading alpha after thread 0 replaced it by v's 1.)
+#ifdef GPR_TESTING
+#define TRD_DELAY(site)                                                                 \
+  do {                                                                                  \
+    if (a.delay > 0 && ((int)blockIdx.x + (int)(threadIdx.x >> 6) + (site) + j) % 3 == 0) \
+      for (int q_ = 0; q_ < a.delay; ++q_) __builtin_amdgcn_s_sleep(127);              \
+  } while (0)
+#else
+#define TRD_DELAY(site) \
+  do {                  \
+  } while (0)
+#endif
+
 #ifdef GPR_TESTING
 // phase stamps of workgroups 0 and P-1 (test build only: tools/trd_trace.py)
 __device__ long long g_trd_trace[2][TRD_MAXN][6];
@@ -119,6 +137,7 @@ struct TrdArgs {
   long long spin_limit;
 #ifdef GPR_TESTING
   int fail_step;    // (test build) workgroup 0 never publishes its partial sum of this step
+  int delay;        // (test build) GPR_TRD_DELAY: late-wave injection, see trd_delay
 #endif
   double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
   size_t ldb;
@@ -222,6 +241,9 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
   {  // v_0 from column 0 (no update before it), redundantly in every workgroup
     double beta;
     double d0;
+    const int j = 0;
+    (void)j;
+    TRD_DELAY(0);  // (a late wave reading dlarfg's alpha)
     if (GV) {  // column 0 of the work copy is never updated: read it in place, write V's
       d0 = a.A[0];
       tj = trd_reflector(n, 0, a.A, a.V, red, &beta);
@@ -300,6 +322,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     // ---- publish this workgroup's part of p_j . v_j (no arrival counter: every handed-off
     // value is its own flag, see the exchange)
     TRD_STAMP(1);
+    TRD_DELAY(1);  // (a late writer of the wave partial sums)
     if (lane == 0) red[wv] = sp;
     __syncthreads();
     TRD_WGSTAMP(1);  // (every wave's pass done)
@@ -374,6 +397,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     const double* pj = a.pbuf + (size_t)j * a.lda;
     const double* cp = a.cpub + (size_t)(j + 1) * a.lda;
     const double* pp = a.parts + (size_t)j * P;
+    TRD_DELAY(2);  // (workgroups arriving late at the exchange: the sentinel protocol)
     double xn = 0.0;
     if constexpr (!GV) {
       double pr[RP], cr[RP];
@@ -473,6 +497,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       // dlarfg on cnew[j+2..n-1] -> v_{j+1} in place
       // alpha from its own LDS slot, not cnew[j + 2]: thread 0 overwrites that entry with v's
       // leading 1 below, possibly before another wave has read it (no barrier in between)
+      TRD_DELAY(3);  // (a late reader of alpha, after another wave's v stores)
       const double alpha = *s_alpha;
       double tau = 0.0, beta = alpha, scal = 0.0;
       if (xnorm2 > 0.0) {
@@ -491,6 +516,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
         a.tau[j + 1] = tau;
       }
       tj = tau;
+      TRD_DELAY(4);  // (a late writer of v_{j+1} before the next pass reads it)
       __syncthreads();
     } else if (out && tid == 0) {  // the last 2 x 2 block: e_{n-2}, d_{n-1}
       a.e[n - 2] = cnew[n - 1];
@@ -836,6 +862,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   // shortens the bound so the time-out comes quickly)
   a.fail_step = getenv("GPR_TRD_FAIL_STEP") ? atoi(getenv("GPR_TRD_FAIL_STEP")) : -1;
   if (const char* e = getenv("GPR_TRD_SPIN_LIMIT")) a.spin_limit = atoll(e);
+  a.delay = getenv("GPR_TRD_DELAY") ? std::max(0, atoi(getenv("GPR_TRD_DELAY"))) : 0;
 #endif
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;

@@ -405,3 +405,26 @@ def test_syev_and_sytrd_padded_leading_dimensions(n, m):
     np.testing.assert_array_equal(ctx.host(de)[:n - 1], e0)
     np.testing.assert_array_equal(ctx.host(dB2)[:n], Q0)
     assert (ctx.host(dB2)[n:] == -3.0).all()
+
+
+def test_eigen_suite_under_injected_delays():
+    """This file's tests once more, in a child process on the test build libgpr_hip_testing.so
+    with late-wave injection in the reduction and the divide and conquer (GPR_TRD_DELAY /
+    GPR_DC_DELAY: one wave in three sleeps before each read that follows another wave's LDS or
+    global write, and before each hand-off poll -- DESIGN.md section 7's audit lists every such
+    slot and what orders it).  The schedule that exposed round 5's dlarfg alpha race (a wave
+    reading alpha after thread 0 had replaced it) is forced here on every step, so a missing
+    barrier or flag gives wrong results deterministically instead of one run in three."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT, TESTING_LIB
+    env = dict(os.environ, GPR_HIP_LIB=TESTING_LIB, GPR_TRD_DELAY="1", GPR_DC_DELAY="1")
+    for k in ("GPR_TRD_FAIL_STEP", "GPR_TRD_SPIN_LIMIT", "GPR_TRD_QCHUNK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_eigen.py"),
+                        "-k", "not injected_delays and not timeout and not rocsolver"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout

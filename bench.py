@@ -281,6 +281,33 @@ def _cpu_baseline_at(a, kinds, hp, n, m, threads):
     }
 
 
+def store_ceiling(lib, ctx, K, n):
+    """Pure-store ceilings of the fit's upper-only K build (bench instrumentation,
+    csrc/probe/store_ceiling.hip): the kernel's own write shape (persistent grid, 4 columns x
+    128 B per store instruction), the same items one wave each, and 1-KB column chunks in
+    column order one per wave -- best of 3 after a warm-up each, on the bench's K buffer."""
+    path = os.path.join(ROOT, "gaussianprocessregression.jl_amd", "gpr_amd", "libgpr_store_probe.so")
+    if not os.path.exists(path):
+        return None
+    pl = ctypes.CDLL(path)
+    pl.gpr_probe_upper_store.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double)]
+    stream = lib.gpr_ctx_stream(ctx.h)
+    out = {}
+    for pat, name in ((0, "kernel_pattern"), (1, "item_per_wave"), (2, "chunk1k_column_order")):
+        ms, nb = ctypes.c_double(), ctypes.c_double()
+        rc = pl.gpr_probe_upper_store(stream, n, ctypes.c_void_p(K.data_ptr()), pat, 3,
+                                      ctypes.byref(ms), ctypes.byref(nb))
+        if rc != 0:
+            return {"error": f"gpr_probe_upper_store pattern {pat} rc {rc}"}
+        out[name] = {"ms": ms.value, "GBps": nb.value / (ms.value * 1e-3) / 1e9}
+        out["bytes"] = nb.value
+    out["best_GBps"] = max(v["GBps"] for k, v in out.items() if isinstance(v, dict))
+    out["best_hbm_frac"] = out["best_GBps"] / HBM_PEAK_GBS
+    return out
+
+
 class _StdoutToStderr:
     """RCCL prints its banner and warnings to STDOUT from C; the driver reads ONE JSON line
     there.  Point file descriptor 1 at stderr while communicators are created and used, and
@@ -507,6 +534,7 @@ def main():
             if rc < 0:  # (rc > 0, K not positive definite, still timed the build)
                 break
             kb_se = cls_get(0)
+    ceiling = store_ceiling(lib, ctx, K, N) if not a.no_se_ard else None
     names = ["kbuild", "potrf", "potrs", "posterior"]
     for i, nm in enumerate(names):
         stg[nm] = e[i].elapsed_time(e[i + 1])
@@ -562,7 +590,12 @@ def main():
                 "GBps": kb_se[2] / (kb_se[0] * 1e-3) / 1e9,
                 "hbm_frac": kb_se[2] / (kb_se[0] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "note": "the fit's upper-only K build for SE-ARD (configs[1]'s kernel) at this "
-                        "N and d, timed inside gpr_fit; not the headline kernel"},
+                        "N and d, timed inside gpr_fit; not the headline kernel",
+                "frac_of_store_ceiling": (None if not ceiling else
+                                          kb_se[2] / (kb_se[0] * 1e-3) / 1e9 / ceiling["best_GBps"])},
+            # the same bytes written with no arithmetic, same box and process (pure-store kernels of
+            # libgpr_store_probe.so): the store rate any upper-only K build is bounded by
+            "kbuild_store_ceiling": ceiling,
             "potrf_TFLOPs": potrf_tf,
             "potrf_mfma_frac": potrf_tf / FP64_MFMA_PEAK,
             "stage_ms_unfused": stg,

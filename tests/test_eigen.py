@@ -16,6 +16,7 @@ on random symmetric matrices (ragged sizes, 1 to 1100) and on the reference's ow
 matrices (ill-conditioned, clustered spectra).  The oracle here is numpy's LAPACK.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -133,9 +134,10 @@ def test_integrate_noise_native_routes_vs_oracle(quad, knobs):
     Io, vo = O.integrate_noise(kinds, hp, x, Y, a, b, noise)
     np.testing.assert_allclose(I, Io, rtol=1e-8)
     np.testing.assert_allclose(v, vo, rtol=1e-7, atol=1e-12 * O.antideriv2_se(hp, a, b))
-    knobs("GPR_QUAD_EIGEN", 2)
-    with pytest.raises(G.GprError, match="test build"):
-        G.integrate(md, a, b, sample_noise=noise)
+    if os.path.basename(G._lib.LIB_PATH) == "libgpr_hip.so":  # (the release build)
+        knobs("GPR_QUAD_EIGEN", 2)
+        with pytest.raises(G.GprError, match="test build"):
+            G.integrate(md, a, b, sample_noise=noise)
 
 
 def test_integrate_noise_rocsolver_comparator_test_build():

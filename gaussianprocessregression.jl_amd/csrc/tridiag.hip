@@ -659,19 +659,23 @@ __global__ __launch_bounds__(QB) void qblock_t_kernel(const double* __restrict__
 // elimination with partial pivoting on the tridiagonal (dgtsv: the row interchanges fill a
 // second superdiagonal), then out[2j] = C[:, j] . x (= k1' (K + s_j I)^{-1} y_j, Iout) and
 // out[2j+1] = k2 - c . x (var).  Columns [j0, j1) of this launch; scratch: 4 n doubles per
-// column of the launch.
+// column of the launch, interleaved across the launch's columns (entry i of array k of column
+// t at scr[(k n + i) cols + t]) so a wave's 64 columns touch 64 consecutive doubles per step
+// (d, e and c are the same for every column: broadcast loads).
 __global__ void quad_tridiag_kernel(const double* __restrict__ d, const double* __restrict__ e,
                                     int n, const double* __restrict__ C, size_t ldc, int ny,
                                     int j0, int j1, const double* __restrict__ noise, double k2,
                                     double* __restrict__ scr, double* __restrict__ out) {
-  const int j = j0 + blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = j0 + t;
   if (j >= j1) return;
+  const size_t cols = (size_t)(j1 - j0);
   const double s = noise[j];
   const double* c = C + (size_t)ny * ldc;
-  double* Dm = scr + (size_t)(j - j0) * 4 * n;  // final pivots
-  double* U1 = Dm + n;                   // first superdiagonal
-  double* U2 = U1 + n;                   // second superdiagonal (row interchanges)
-  double* x = U2 + n;                    // right-hand side -> solution
+  double* Dm = scr + t;                   // final pivots: Dm[i cols]
+  double* U1 = Dm + (size_t)n * cols;     // first superdiagonal
+  double* U2 = U1 + (size_t)n * cols;     // second superdiagonal (row interchanges)
+  double* x = U2 + (size_t)n * cols;      // right-hand side -> solution
   if (n == 1) {
     const double x0 = c[0] / (d[0] + s);
     out[2 * j] = C[(size_t)j * ldc] * x0;
@@ -681,25 +685,26 @@ __global__ void quad_tridiag_kernel(const double* __restrict__ d, const double* 
   // running row i: (Di, Ui) on the diagonal / superdiagonal, bi; next row: (L = e_i, Dn, Un)
   double Di = d[0] + s, Ui = e[0], bi = c[0];
   for (int i = 0; i < n - 1; ++i) {
+    const size_t at = (size_t)i * cols;
     const double L = e[i];
     const double Dn = d[i + 1] + s;
     const double Un = i + 1 < n - 1 ? e[i + 1] : 0.0;
     const double bn = c[i + 1];
     if (fabs(Di) >= fabs(L)) {  // no interchange
       const double f = L / Di;
-      Dm[i] = Di;
-      U1[i] = Ui;
-      U2[i] = 0.0;
-      x[i] = bi;
+      Dm[at] = Di;
+      U1[at] = Ui;
+      U2[at] = 0.0;
+      x[at] = bi;
       Di = Dn - f * Ui;
       Ui = Un;
       bi = bn - f * bi;
     } else {  // rows i and i + 1 swap: row i becomes (L, Dn, Un), the next (Di, Ui, 0) - f row i
       const double f = Di / L;
-      Dm[i] = L;
-      U1[i] = Dn;
-      U2[i] = Un;
-      x[i] = bn;
+      Dm[at] = L;
+      U1[at] = Dn;
+      U2[at] = Un;
+      x[at] = bn;
       const double nd = Ui - f * Dn;
       const double nu = -f * Un;
       const double nb = bi - f * bn;
@@ -708,14 +713,13 @@ __global__ void quad_tridiag_kernel(const double* __restrict__ d, const double* 
       bi = nb;
     }
   }
-  Dm[n - 1] = Di;
-  x[n - 1] = bi;
   // back substitution, dotting as it goes
   const double* cy = C + (size_t)j * ldc;
   double x2 = 0.0, x1 = bi / Di;
   double si = cy[n - 1] * x1, sv = c[n - 1] * x1;
   for (int i = n - 2; i >= 0; --i) {
-    const double xi = (x[i] - U1[i] * x1 - U2[i] * x2) / Dm[i];
+    const size_t at = (size_t)i * cols;
+    const double xi = (x[at] - U1[at] * x1 - U2[at] * x2) / Dm[at];
     si += cy[i] * xi;
     sv += c[i] * xi;
     x2 = x1;

@@ -295,7 +295,8 @@ def store_ceiling(lib, ctx, K, n):
                                          ctypes.POINTER(ctypes.c_double)]
     stream = lib.gpr_ctx_stream(ctx.h)
     out = {}
-    for pat, name in ((0, "kernel_pattern"), (1, "item_per_wave"), (2, "chunk1k_column_order")):
+    for pat, name in ((0, "kernel_pattern"), (1, "item_per_wave"), (2, "chunk1k_column_order"),
+                      (3, "items_1k_column_stores"), (4, "items16_1k_column_stores")):
         ms, nb = ctypes.c_double(), ctypes.c_double()
         rc = pl.gpr_probe_upper_store(stream, n, ctypes.c_void_p(K.data_ptr()), pat, 3,
                                       ctypes.byref(ms), ctypes.byref(nb))

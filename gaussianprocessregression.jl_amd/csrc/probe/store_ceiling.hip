@@ -9,6 +9,9 @@
 //   pattern 1  the same items, one wave per item (no persistent loop: dispatch order)
 //   pattern 2  1-KB column chunks in column order, one chunk per wave (16-B stores: each
 //              instruction one column's 128 rows) -- the fastest upper-only order measured
+//   pattern 3  the kernel's items and persistent grid, but each store instruction one column's
+//              128 rows (1 KB, 16-B lanes): what an LDS-transposed D layout would write
+//   pattern 4  as 3 with 16-column strips
 // Each is launched `reps` times after one warm-up; the best time is returned.
 #include <hip/hip_runtime.h>
 
@@ -42,6 +45,26 @@ __global__ __launch_bounds__(256) void st_kup(double* K, int n, size_t ld, const
   }
 }
 
+template <int W>
+__global__ __launch_bounds__(256) void st_kup_col(double* K, int n, size_t ld, const int* items,
+                                                  int nitems, double v) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nitems; t += gridDim.x * 4) {
+    const int code = items[t];
+    const int j0 = (code >> 16) * W, r0 = (code & 0xffff) * 128;
+    const int r1 = min(r0 + 128, up_rows(j0, n));
+    const int r = r0 + 2 * lane;
+#pragma unroll 4
+    for (int c = j0; c < min(j0 + W, n); ++c) {
+      if (r + 1 < r1)
+        __builtin_nontemporal_store(d2{v, v}, reinterpret_cast<d2*>(K + (size_t)r + (size_t)c * ld));
+      else if (r < r1)
+        __builtin_nontemporal_store(v, K + (size_t)r + (size_t)c * ld);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void st_flat(double* K, int n, size_t ld,
                                                const long long* chunks, int nch, double v) {
   typedef double d2 __attribute__((ext_vector_type(2)));
@@ -65,15 +88,16 @@ extern "C" {
 // time (ms) and the bytes written per launch; negative on a HIP error.
 int gpr_probe_upper_store(void* stream, int n, double* K, int pattern, int reps, double* best_ms,
                           double* bytes) {
-  if (n <= 0 || !K || !best_ms || !bytes || pattern < 0 || pattern > 2) return -1;
+  if (n <= 0 || !K || !best_ms || !bytes || pattern < 0 || pattern > 4) return -1;
   hipStream_t s = (hipStream_t)stream;
   const size_t ld = (size_t)n;
   std::vector<int> items;
   std::vector<long long> chunks;
+  const int W = pattern == 4 ? 16 : 32;
   double nb = 0.0;
   for (int c = 0; c < n; ++c) nb += 8.0 * up_rows(c, n);
-  for (int bj = 0; bj * 32 < n; ++bj)
-    for (int sg = 0; sg * 128 < up_rows(bj * 32, n); ++sg) items.push_back((bj << 16) | sg);
+  for (int bj = 0; bj * W < n; ++bj)
+    for (int sg = 0; sg * 128 < up_rows(bj * W, n); ++sg) items.push_back((bj << 16) | sg);
   for (int c = 0; c < n; ++c)
     for (int r = 0; r < up_rows(c, n); r += 128) chunks.push_back(((long long)c << 20) | r);
   int* ditems = nullptr;
@@ -94,8 +118,12 @@ int gpr_probe_upper_store(void* stream, int n, double* K, int pattern, int reps,
       st_kup<<<std::max(1, std::min((nit + 3) / 4, 256 * 8)), 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
     else if (pattern == 1)
       st_kup<<<(nit + 3) / 4, 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
-    else
+    else if (pattern == 2)
       st_flat<<<(nch + 3) / 4, 256, 0, s>>>(K, n, ld, dch, nch, 1.0);
+    else if (pattern == 3)
+      st_kup_col<32><<<std::max(1, std::min((nit + 3) / 4, 256 * 8)), 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
+    else
+      st_kup_col<16><<<std::max(1, std::min((nit + 3) / 4, 256 * 8)), 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
     float ms = 0.f;

@@ -876,14 +876,69 @@ __device__ __forceinline__ void kup_unit(const KParams& kp, const double (&ca)[N
   }
 }
 
+// One interior item of a single-part build (NSE = 1: 32 columns x KU_SEG rows, no diagonal
+// element, no ragged edge; GPR_KBUILD_COLSTORE), its values staged through this wave's LDS 16
+// columns at a time and stored as one column's 128 rows per store instruction (1 KB, 16 B per
+// lane) instead of the MFMA D layout's 4 columns x 128 B: the fastest upper-only store shape the
+// kernel's items allow (bench.py `kbuild_store_ceiling`: items_1k_column_stores).  The same
+// MFMAs and exponentials as kup_unit in the same order per element: bit for bit the same K.
+constexpr int KU_SP = KU_SEG + 2;  // staging column stride (doubles): +16 B against bank repeats
+template <int S, bool CLAMP>
+__device__ __forceinline__ void kup_item_cols(const double (&ca)[1][KU_CB][S], const double* cn,
+                                              const double* __restrict__ gA,
+                                              const double* __restrict__ nrm, const double* tabs,
+                                              double* stg, double* __restrict__ K, size_t ldk,
+                                              int r0, int j0) {
+  constexpr int RB = KU_SEG / 16;  // row blocks of the item
+  const int lane = threadIdx.x & 63;
+  double ra[RB][S], rn[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int ba = (r0 >> 4) + rb;
+#pragma unroll
+    for (int s = 0; s < S; ++s) ra[rb][s] = gA[((size_t)ba * S + s) * 64 + lane];
+    rn[rb] = nrm[ba * 16 + (lane & 15)];
+  }
+#pragma unroll
+  for (int cb = 0; cb < KU_CB; ++cb) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      gd4 acc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = rn[rb] + cn[16 * cb + (lane >> 4) + 4 * q];
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[0][cb][s], ra[rb][s], acc, 0, 0, 0);
+      double e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) e[q] = CLAMP ? kexp_s2(-acc[q], tabs) : kexp_s2_nc(-acc[q], tabs);
+      asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) stg[((lane >> 4) + 4 * q) * KU_SP + 16 * rb + (lane & 15)] = e[q];
+    }
+    // (one wave's LDS operations complete in order: the reads below see the writes above)
+#pragma unroll 4
+    for (int c = 0; c < 16; ++c) {
+      const kd2 v = *reinterpret_cast<const kd2*>(stg + c * KU_SP + 2 * lane);
+      double* dst = K + (size_t)r0 + 2 * lane + (size_t)(j0 + 16 * cb + c) * ldk;
+#ifdef GPR_KBUILD_NOSTORE  // diagnostics (tools/kbuild_bench_nostore): compute-only timing
+      if (!(v.x == v.x)) *dst = v.x;
+#else
+      __builtin_nontemporal_store(v, reinterpret_cast<kd2*>(dst));
+#endif
+    }
+  }
+}
+
 template <int S, int NSE>
 __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, const double* __restrict__ gA,
                                                         const double* __restrict__ gB,
                                                         const double* __restrict__ nrm, int nblk,
                                                         int n, double* __restrict__ K, size_t ldk,
                                                         const int* __restrict__ items, int nitems,
-                                                        int full) {
+                                                        int full, int colstore) {
   extern __shared__ double tabs[];  // NSE exp tables, then per wave the strip's column norms
+                                    // (then, colstore, per wave the 16-column staging)
   load_part_tables(kp, tabs);
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -919,6 +974,21 @@ __global__ __launch_bounds__(256, KU_MINB) void kmat_symu_kernel(KParams kp, con
       }
     const bool cols_big = __ballot(big) != 0;
     __builtin_amdgcn_wave_barrier();
+    if constexpr (NSE == 1) {
+      // an interior item (a full segment of rows, every column inside n, no diagonal element)
+      // through the column-store path
+      if (colstore && r1 - r0 == KU_SEG && j0 + KU_W <= n && !(j0 >= r0 && j0 < r1)) {
+        double* stg = tabs + (256 + 4 * KU_W) * NSE + (threadIdx.x >> 6) * (16 * KU_SP);
+        bool rbig = cols_big;
+        for (int rb = 0; rb < KU_SEG / 16; ++rb)
+          rbig |= !(-nrm[(r0 >> 4) * 16 + rb * 16 + (lane & 15)] < KU_NC_LIM);
+        if (__ballot(rbig) != 0)
+          kup_item_cols<S, true>(ca, cn, gA, nrm, tabs, stg, K, ldk, r0, j0);
+        else
+          kup_item_cols<S, false>(ca, cn, gA, nrm, tabs, stg, K, ldk, r0, j0);
+        continue;
+      }
+    }
     // row operands (B role) of a 32-row unit: clamped to the last unit (branch-free prefetch)
     auto load_rows = [&](int i0, double (&ra)[NSE][2][S], double (&rn)[NSE][2]) {
       const int ii = min(i0, r1 - 1) & ~(KU_H - 1);
@@ -1080,8 +1150,15 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
   }
   LAUNCH_CHECK(ctx);
   const int grid = std::max(1, std::min((kl->nitems + 3) / 4, 256 * wgs));
-  kmat_symu_kernel<S, NSE><<<grid, 256, sizeof(double) * (256 + 4 * KU_W) * NSE, ctx->stream>>>(
-      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, kl->d, kl->nitems, full);
+  // GPR_KBUILD_COLSTORE (single-part builds): interior items stored a column's 128 rows per
+  // instruction through 16.6 KB of LDS per wave (16-B stores: K 16-B aligned, ldk even)
+  // (the fit's upper-only build only: for the full column build of gpr_kernel it measured 6 %
+  // slower, 1.73-1.76 vs 1.63-1.65 ms at N = 32768, profiles/r06_kbuild_colstore_ab.txt)
+  const int colstore = NSE == 1 && !full && ctx->kbuild_colstore && (ldk % 2) == 0 &&
+                       ((uintptr_t)K % 16) == 0;
+  const size_t lds = sizeof(double) * ((256 + 4 * KU_W) * NSE + (colstore ? 4 * 16 * KU_SP : 0));
+  kmat_symu_kernel<S, NSE><<<grid, 256, lds, ctx->stream>>>(
+      kp, A, B, nrmA, nbA, n, K, (size_t)ldk, kl->d, kl->nitems, full, colstore);
   LAUNCH_CHECK(ctx);
   return 0;
 }

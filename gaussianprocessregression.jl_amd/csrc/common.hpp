@@ -184,6 +184,8 @@ struct gpr_ctx {
   size_t tri_cap = 0;
   int kbuild_upper = 1;         // GPR_KBUILD_UPPER=0: fits build the full K (mirrored tiles)
   int kbuild_exact = 0;         // GPR_KBUILD_EXACT=1: the reference's difference form for K
+  int kbuild_colstore = 1;      // GPR_KBUILD_COLSTORE=0: single-part upper builds store in the
+                                // MFMA D layout instead of 1-KB column segments
   int cv_batch = 1;             // GPR_CV_BATCH=0: cv_batch folds one by one on child contexts
   double cv_batch_gb = 16.0;    // GPR_CV_BATCH_GB: device-memory budget of a batched launch
   double quad_batch_gb = 16.0;  // GPR_QUAD_BATCH_GB: the same for the quadrature's columns

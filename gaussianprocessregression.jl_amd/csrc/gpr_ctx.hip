@@ -145,6 +145,7 @@ const Knob kKnobs[] = {
     {"GPR_FUSE_KINV", &gpr_ctx::fuse_kinv, nullptr},
     {"GPR_KBUILD_UPPER", &gpr_ctx::kbuild_upper, nullptr},
     {"GPR_KBUILD_EXACT", &gpr_ctx::kbuild_exact, nullptr},
+    {"GPR_KBUILD_COLSTORE", &gpr_ctx::kbuild_colstore, nullptr},
     {"GPR_CV_STREAMS", &gpr_ctx::cv_streams, nullptr},
     {"GPR_CV_BATCH", &gpr_ctx::cv_batch, nullptr},
     {"GPR_CV_BATCH_GB", nullptr, &gpr_ctx::cv_batch_gb},

@@ -101,6 +101,8 @@ int gpr_set_outer_block(gpr_ctx_t ctx, int nb2);
  *   GPR_FUSE_KINV     -1  gpr_fit_kinv: Z (1) and Z^T Z (2) inside the factorisation (-1 = 2)
  *   GPR_KBUILD_UPPER   1  fits assemble only what dpotrf 'U' reads (the DAG mirrors the rest)
  *   GPR_KBUILD_EXACT   0  1: K by the reference's difference form instead of the Gram form
+ *   GPR_KBUILD_COLSTORE 1 single-part (SE) upper builds store 1-KB column segments through LDS;
+ *                         0: the MFMA D layout (4 columns x 128 B per store instruction)
  *   GPR_CV_BATCH       1  gpr_cv_batch: every fold in one batched launch; 0: per fold
  *   GPR_CV_BATCH_GB   16  device-memory budget of one batched cross-validation launch
  *   GPR_CV_STREAMS     4  child contexts of the per-fold / per-column paths (<= 8)

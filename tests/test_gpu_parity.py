@@ -1128,3 +1128,35 @@ def test_fit_buffer_not_posdef_keeps_lower_k(eps, fails_at):
     assert rc == info.value == fails_at
     _, Kfull, _ = _ref_buffer(ctx, kinds, hp, x, eps=eps)
     assert np.array_equal(np.tril(ctx.host(K), -1), np.tril(Kfull, -1))
+
+
+@pytest.mark.parametrize("n,dim", [(1040, 8), (2064, 5), (4096, 8), (4100, 3), (4099, 3)])
+def test_kbuild_colstore_bitwise(n, dim, knobs):
+    """GPR_KBUILD_COLSTORE (single-part upper builds of the fits: interior items staged through
+    LDS and stored as 1-KB column segments) changes only the store shape: the fit's buffer
+    (upper U, strict lower K) is bit for bit that of the MFMA-layout stores (and gpr_kernel's
+    full symmetric K, which keeps the MFMA layout, is unchanged by the knob), including the ragged and diagonal items that keep the old path (n = 4100: odd
+    leading dimension -> the 16-B path declines)."""
+    kinds = KSETS["SE"]
+    rng = np.random.default_rng(n * dim)
+    hp = O.default_hp(kinds, dim)
+    x = rng.random((dim, n))
+    y = np.sin(x.sum(0)) ** 2
+    ctx = G.core.default_context()
+    dx, dy = ctx.colmajor(x), ctx.colmajor(y)
+    karr = _karr(kinds)
+    hpp = hp.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    lib = G._lib.lib
+    out = {}
+    for cs in (0, 1):
+        knobs("GPR_KBUILD_COLSTORE", cs)
+        K, alpha = ctx.empty(n, n), ctx.empty(n)
+        info = ctypes.c_int(-7)
+        assert lib.gpr_fit(ctx.h, karr, 1, hpp, dim, _P(dx), n, _P(dy), 1, n, 1e-8, _P(K), n,
+                           _P(alpha), ctypes.byref(info)) == 0 and info.value == 0
+        Kf = ctx.empty(n, n)
+        assert lib.gpr_kernel(ctx.h, karr, 1, hpp, dim, _P(dx), n, None, n, 1, 1e-8, _P(Kf), n) == 0
+        out[cs] = (ctx.host(K).copy(), ctx.host(alpha).copy(), ctx.host(Kf).copy())
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+    np.testing.assert_allclose(out[1][2], O.kernel(kinds, hp, x), rtol=1e-13, atol=1e-300)

@@ -283,9 +283,11 @@ def _cpu_baseline_at(a, kinds, hp, n, m, threads):
 
 def store_ceiling(lib, ctx, K, n):
     """Pure-store ceilings of the fit's upper-only K build (bench instrumentation,
-    csrc/probe/store_ceiling.hip): the kernel's own write shape (persistent grid, 4 columns x
-    128 B per store instruction), the same items one wave each, and 1-KB column chunks in
-    column order one per wave -- best of 3 after a warm-up each, on the bench's K buffer."""
+    csrc/probe/store_ceiling.hip): the MFMA-layout shape (persistent grid, 4 columns x 128 B
+    per store instruction), the same items one wave each, 1-KB column chunks in column order one
+    per wave, the items with 1-KB column stores (persistent; 16-column strips; one item per
+    wave -- the single-part build's own shape since round 6) -- best of 3 after a warm-up each,
+    on the bench's K buffer."""
     path = os.path.join(ROOT, "gaussianprocessregression.jl_amd", "gpr_amd", "libgpr_store_probe.so")
     if not os.path.exists(path):
         return None
@@ -296,7 +298,8 @@ def store_ceiling(lib, ctx, K, n):
     stream = lib.gpr_ctx_stream(ctx.h)
     out = {}
     for pat, name in ((0, "kernel_pattern"), (1, "item_per_wave"), (2, "chunk1k_column_order"),
-                      (3, "items_1k_column_stores"), (4, "items16_1k_column_stores")):
+                      (3, "items_1k_column_stores"), (4, "items16_1k_column_stores"),
+                      (5, "items_1k_column_stores_item_per_wave")):
         ms, nb = ctypes.c_double(), ctypes.c_double()
         rc = pl.gpr_probe_upper_store(stream, n, ctypes.c_void_p(K.data_ptr()), pat, 3,
                                       ctypes.byref(ms), ctypes.byref(nb))

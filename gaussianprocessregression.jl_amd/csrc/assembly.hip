@@ -1094,10 +1094,23 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
   double* A = ctx->dgA;
   double* nrmA = A + opA;
   double* B = nrmA + nA;
-  constexpr int wgs = 8;  // workgroups per CU of the persistent grid
-  // work list, cached per (n, full) in a few slots (fold and prior builds of cross-validation
-  // alternate two shapes): rebuilding one costs a sync, a free and a blocking copy
-  const long long key = 2LL * n + full;
+  // GPR_KBUILD_COLSTORE (single-part builds): interior items stored a column's 128 rows per
+  // instruction through 16.6 KB of LDS per wave (16-B stores: K 16-B aligned, ldk even), and
+  // one item per wave (no persistent loop: the hardware dispatches the items in list order, so
+  // the running waves write a narrow, advancing band of columns).  The fit's upper-only build
+  // only: for the full column build of gpr_kernel the column stores measured 6 % slower (1.73-
+  // 1.76 vs 1.63-1.65 ms at N = 32768).  SE, N = 32768, d = 8, same box (profiles/r06_kbuild_
+  // colstore_ab.txt): MFMA-layout stores 0.85-0.86 ms persistent / 0.82-0.83 one item per wave;
+  // column stores 0.81-0.82 persistent / 0.70-0.72 one item per wave (0.75-0.78 of 8 TB/s).
+  const int colstore = NSE == 1 && !full && ctx->kbuild_colstore && (ldk % 2) == 0 &&
+                       ((uintptr_t)K % 16) == 0;
+#ifndef KU_WGS  // workgroups per CU of the persistent grid (diagnostic builds: 1 << 20 = one
+#define KU_WGS 8  // item per wave, dispatch order)
+#endif
+  const int wgs = colstore ? (1 << 20) : KU_WGS;  // workgroups per CU of the grid
+  // work list, cached per (n, full, grid shape) in a few slots (fold and prior builds of
+  // cross-validation alternate two shapes): rebuilding one costs a sync, a free and a copy
+  const long long key = 4LL * n + 2 * colstore + full;
   gpr_ctx::KupList* kl = nullptr;
   for (auto& e : ctx->kup)
     if (e.key == key) kl = &e;
@@ -1118,7 +1131,7 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
       // streaming all of them through it for every strip.  (Placement is a speed hint only:
       // any order computes the same values.)
       const int nit = (int)items.size();
-      const int W = 4 * std::max(1, std::min((nit + 3) / 4, 256 * wgs));
+      const int W = (int)(4 * std::max(1LL, std::min((long long)(nit + 3) / 4, 256LL * wgs)));
       std::vector<int> q[8];
       for (int it : items) q[(it & 0xffff) % 8].push_back(it);
       size_t pos[8] = {};
@@ -1149,13 +1162,7 @@ int launch_gram_upper(gpr_ctx* ctx, const KParams& kp, const double* xs, int n, 
     gram_prep_kernel<<<blocks, 256, 0, ctx->stream>>>(xs, n, d, S, nbA, NSE, ctx->dgc, 1.0, B, nullptr);
   }
   LAUNCH_CHECK(ctx);
-  const int grid = std::max(1, std::min((kl->nitems + 3) / 4, 256 * wgs));
-  // GPR_KBUILD_COLSTORE (single-part builds): interior items stored a column's 128 rows per
-  // instruction through 16.6 KB of LDS per wave (16-B stores: K 16-B aligned, ldk even)
-  // (the fit's upper-only build only: for the full column build of gpr_kernel it measured 6 %
-  // slower, 1.73-1.76 vs 1.63-1.65 ms at N = 32768, profiles/r06_kbuild_colstore_ab.txt)
-  const int colstore = NSE == 1 && !full && ctx->kbuild_colstore && (ldk % 2) == 0 &&
-                       ((uintptr_t)K % 16) == 0;
+  const int grid = (int)std::max(1LL, std::min((long long)(kl->nitems + 3) / 4, 256LL * wgs));
   const size_t lds = sizeof(double) * ((256 + 4 * KU_W) * NSE + (colstore ? 4 * 16 * KU_SP : 0));
   kmat_symu_kernel<S, NSE><<<grid, 256, lds, ctx->stream>>>(
       kp, A, B, nrmA, nbA, n, K, (size_t)ldk, kl->d, kl->nitems, full, colstore);

@@ -12,6 +12,8 @@
 //   pattern 3  the kernel's items and persistent grid, but each store instruction one column's
 //              128 rows (1 KB, 16-B lanes): what an LDS-transposed D layout would write
 //   pattern 4  as 3 with 16-column strips
+//   pattern 5  as 3, one item per wave (no persistent loop): the shape of the fit's single-part
+//              build since round 6 (GPR_KBUILD_COLSTORE)
 // Each is launched `reps` times after one warm-up; the best time is returned.
 #include <hip/hip_runtime.h>
 
@@ -88,7 +90,7 @@ extern "C" {
 // time (ms) and the bytes written per launch; negative on a HIP error.
 int gpr_probe_upper_store(void* stream, int n, double* K, int pattern, int reps, double* best_ms,
                           double* bytes) {
-  if (n <= 0 || !K || !best_ms || !bytes || pattern < 0 || pattern > 4) return -1;
+  if (n <= 0 || !K || !best_ms || !bytes || pattern < 0 || pattern > 5) return -1;
   hipStream_t s = (hipStream_t)stream;
   const size_t ld = (size_t)n;
   std::vector<int> items;
@@ -122,8 +124,10 @@ int gpr_probe_upper_store(void* stream, int n, double* K, int pattern, int reps,
       st_flat<<<(nch + 3) / 4, 256, 0, s>>>(K, n, ld, dch, nch, 1.0);
     else if (pattern == 3)
       st_kup_col<32><<<std::max(1, std::min((nit + 3) / 4, 256 * 8)), 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
-    else
+    else if (pattern == 4)
       st_kup_col<16><<<std::max(1, std::min((nit + 3) / 4, 256 * 8)), 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
+    else
+      st_kup_col<32><<<(nit + 3) / 4, 256, 0, s>>>(K, n, ld, ditems, nit, 1.0);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
     float ms = 0.f;

@@ -12,7 +12,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 K = torch.empty(n, n, dtype=torch.float64, device="cuda")
 s = torch.cuda.current_stream()
 names = ["kernel_pattern", "item_per_wave", "chunk1k_column_order", "items_1k_column_stores",
-         "items16_1k_column_stores"]
+         "items16_1k_column_stores", "items_1k_column_stores_item_per_wave"]
 for rnd in range(3):
     for pat, nm in enumerate(names):
         ms, nb = ctypes.c_double(), ctypes.c_double()

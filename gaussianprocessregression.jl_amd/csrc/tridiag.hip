@@ -232,7 +232,9 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   const int n = a.n, P = a.P, w = blockIdx.x, L = a.ldl;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double* red = GV ? lds : lds + 3 * (size_t)L;
+  // (GV: one LDS vector, v_j -- the most read of the three: the pass's dot, the exchange, the B
+  // application -- beside the shared global copies of v_{j-1} and w_{j-1})
+  double* red = GV ? lds + L : lds + 3 * (size_t)L;
   int* s_ok = reinterpret_cast<int*>(red + TRD_WAVES);
   double* s_alpha = red + TRD_WAVES + 1;  // column j+1's entry j+2 after step j (dlarfg's alpha)
   int ivp = 0, iwp = 1, ivc = 2;
@@ -247,6 +249,8 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     if (GV) {  // column 0 of the work copy is never updated: read it in place, write V's
       d0 = a.A[0];
       tj = trd_reflector(n, 0, a.A, a.V, red, &beta);
+      for (int r = 1 + tid; r < n; r += TRD_THREADS) lds[r] = a.V[r];  // (own writes, after
+      __syncthreads();                                                 //  the reflector's barrier)
     } else {
       double* c = lds + (size_t)ivc * L;
       for (int r = tid; r < n; r += TRD_THREADS) c[r] = a.A[r];
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     const double* vprev = GV ? a.V + (size_t)(j > 0 ? j - 1 : 0) * a.lda : lds + (size_t)ivp * L;
     const double* wprev = GV ? (j > 0 ? a.wr + (size_t)((j - 1) & 3) * a.lda : a.V)
                              : lds + (size_t)iwp * L;
-    const double* vcur = GV ? a.V + (size_t)j * a.lda : lds + (size_t)ivc * L;
+    const double* vcur = GV ? lds : lds + (size_t)ivc * L;
     // ---- the pass over this workgroup's columns c > j, one wave per column: rows from the
     // even r0 <= j + 1 (16-B accesses; row j, when included, is never read again), PU row pairs
     // in flight per lane
@@ -509,6 +513,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
       for (int r = j + 2 + tid; r < n; r += TRD_THREADS) {
         const double v = r == j + 2 ? 1.0 : cnew[r] * scal;
         vnext[r] = v;
+        if (GV) lds[r] = v;  // (v_j's reads in this step all precede block_sum's barriers)
         if (out && !GV) vj[r] = v;
       }
       if (out && tid == 0) {
@@ -788,7 +793,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 #ifdef GPR_TESTING
   if (const char* e = getenv("GPR_TRD_COLS")) cols = std::max(1, atoi(e));  // (tuning sweeps)
 #endif
-  const size_t shmem = ((gv ? 0 : 3 * (size_t)((n + 1) & ~1)) + TRD_WAVES + 2) * sizeof(double);
+  const size_t shmem = ((gv ? 1 : 3) * (size_t)((n + 1) & ~1) + TRD_WAVES + 2) * sizeof(double);
   const void* kfn = gv ? trd_kernel_ptr<16, RPT_G, true>()
                        : n >= 800 ? trd_kernel_ptr<16, RPT, false>() : trd_kernel_ptr<8, RPT, false>();
   // co-residency: one workgroup per CU (the launch bound and, for the LDS variant, its vectors

@@ -285,13 +285,16 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  *    never info > 0 (an indefinite K + noise_j I gives the reference's indefinite solve);
  *  - the K + noise_j I factored per column, all in one batched tile-DAG launch that also solves
  *    U_j^{-T} [y_j | k1] (same result within rounding), while that is measured to cost less
- *    (ny below ~200 at n = 4096, ~240 at 2048, ~380 at 1100, ~770 at 512; always beyond the
- *    reduction's bound n > 6144); a factorisation that fails (a shift at or below
- *    -lambda_min(K)) hands the call to the reduction, so the default never returns info > 0.
+ *    (ny below ~200 at n = 4096, ~240 at 2048, ~380 at 1100, ~770 at 512, ~290 at 8192;
+ *    always beyond the reduction's bound n > 16384); a factorisation that fails (a shift at or
+ *    below -lambda_min(K)) hands the call to the reduction, so the default never returns
+ *    info > 0 up to that bound.  A reduction whose cooperative launch the runtime refuses (its
+ *    workgroups cannot all be resident) falls back to the factorisations.
  * GPR_QUAD_EIGEN forces a route: 1 the reduction; 3 the reference's full decomposition
  * (reduction + divide and conquer, gpr_syev_apply) and its diagonal updates; 0 always the
  * factorisations (positive definite shifts only; info > 0 -- PosDefException -- otherwise);
- * 2 rocSOLVER dsyevd (dlopen'd) -- a timing comparator, not the product path. */
+ * 2 rocSOLVER dsyevd -- a timing comparator compiled into the test build libgpr_hip_testing.so
+ * only (GPR_E_ARG here). */
 int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int d,
                         const double* dX, int n, const double* dy, int ny, int ldy,
                         const double* a, const double* b, const double* noise, double eps,
@@ -303,8 +306,8 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
  * particular order -- and dB (n x m, ld ldb, device) holds P' B, its rows in the order of
  * dlam.  FP64, as dsyevd: the tridiagonal reduction (gpr_sytrd_apply, B <- Q' B) then Cuppen's
  * divide and conquer on T (deflation, secular equations, Gu-Eisenstat vectors; Z never formed:
- * B <- Z' B merge by merge).  n > 6144: two-sided block Jacobi (32-wide blocks, parallel
- * ordering).  *sweeps (may be NULL) = merge levels (Jacobi: sweeps used).  GPR_E_HIP if Jacobi
+ * B <- Z' B merge by merge).  n > 16384, or a reduction whose cooperative launch is refused:
+ * two-sided block Jacobi (32-wide blocks, parallel ordering).  *sweeps (may be NULL) = merge levels (Jacobi: sweeps used).  GPR_E_HIP if Jacobi
  * does not converge within 60 sweeps. */
 int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                    double* dlam, int* sweeps);
@@ -314,7 +317,9 @@ int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, 
  * dd[n] its diagonal, de[n-1] its off-diagonal (device), and, when m > 0, dB (n x m, ld ldb)
  * <- Q^T dB.  One persistent launch (the unblocked two-sided Householder reduction, columns
  * dealt round-robin over the CUs; for m <= 1024 Q^T B is formed inside it), else the
- * back-transform by 64-reflector blocks on the MFMA GEMM.  n <= 6144 (GPR_E_UNSUP beyond). */
+ * back-transform by 64-reflector blocks on the MFMA GEMM.  The launch is cooperative (every
+ * workgroup resident or refused up front: GPR_E_UNSUP, nothing touched); its step vectors sit
+ * in LDS up to n = 6144 and in global memory beyond.  n <= 16384 (GPR_E_UNSUP beyond). */
 int gpr_sytrd_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,
                     double* dd, double* de);
 

@@ -100,3 +100,23 @@ def test_bench_gpus2_spawns_two_ranks():
     assert '"split_predict"' in r.stderr
     split = [json.loads(x) for x in r.stderr.splitlines() if x.startswith('{"split_predict"')]
     assert split and split[-1]["split_predict"]["n_gpus"] == 2, split
+
+
+def test_workload_label_names_the_config():
+    """bench.py labels its line with the BASELINE config it ran (review r05: the C2 run was
+    labelled C3): C2 = SE-ARD N = 8192 d = 8, C3 = SE+SE+WN N = 32768 d = 8, else custom."""
+    import types
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    ns = {}
+    start = src.index("def config_label(a):")
+    end = src.index("def kinds_of(name):")
+    exec(compile(src[start:end], "bench.py", "exec"), ns)  # (the pure function only: no torch)
+    lab = ns["config_label"]
+    A = lambda k, n, d: types.SimpleNamespace(kernel=k, n=n, d=d)  # noqa: E731
+    assert lab(A("SE", 8192, 8)) == "C2"
+    assert lab(A("SE+SE+WN", 32768, 8)) == "C3"
+    assert lab(A("SE", 32768, 8)) == "custom"
+    assert lab(A("SE+SE+WN", 4096, 8)) == "custom"
+    assert spec is not None

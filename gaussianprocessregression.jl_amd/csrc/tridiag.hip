@@ -147,6 +147,13 @@ struct TrdArgs {
   // column j + 1 after step j in rings of 4 columns (ld lda): wr[(j & 3) lda], xr[(j & 3) lda]
   double* wr;
   double* xr;
+  int nt;           // GV pass: non-temporal column loads (bit 0) / stores (bit 1)
+  // DF variant (deferred updates, sytrd_df_kernel): w_k in Wv's column k (every workgroup writes
+  // the same bits), the panel's dot-product partials in abuf (n x 2 DF_NB x P, each written once),
+  // deferred panels for steps j < jt, ncl = ceil(n / P) columns per workgroup
+  double* Wv;
+  double* abuf;
+  int jt, ncl;
 };
 
 // workgroup sum of one value per thread (red: >= TRD_WAVES doubles of LDS), deterministic: the
@@ -292,7 +299,9 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
           const int r = rb + 128 * u;
-          if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
+          if (r < n)
+            x[u] = (GV && (a.nt & 1)) ? __builtin_nontemporal_load(reinterpret_cast<const d2*>(col + r))
+                                      : *reinterpret_cast<const d2*>(col + r);
         }
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
@@ -304,7 +313,8 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
             if (j > 0) {
               x[u].x -= vp.x * wc + wp.x * vc;
               x[u].y -= vp.y * wc + wp.y * vc;
-              *reinterpret_cast<d2*>(col + r) = x[u];
+              if (GV && (a.nt & 2)) __builtin_nontemporal_store(x[u], reinterpret_cast<d2*>(col + r));
+              else *reinterpret_cast<d2*>(col + r) = x[u];
             }
             if (pub) {
               st1(pub + r, x[u].x);
@@ -538,6 +548,389 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     ivp = ivc;
     ivc = iwp;
     iwp = t;
+  }
+}
+
+// ---- DF: the reduction with deferred updates (n > TRD_MAXN) ------------------------------
+// The pass above reads AND writes every trailing column every step (16 (n - j)^2 bytes): at n =
+// 8192 that is ~75 % of the launch, at ~4 TB/s.  DF applies the rank-2 updates by panels of
+// DF_NB steps instead (LAPACK's dlatrd idea, inside the same persistent launch):
+//   * step j of a panel [j0, j0 + DF_NB): the columns the panel will publish, (j, j0 + DF_NB], are
+//     kept up to date as before (eager: read, update, write); every later column is only READ,
+//     A(:, c) . v_j, and corrected by the panel's pending updates
+//        p_j[c] = tau_j (A(:, c) . v_j - sum_k (w_k[c] alpha_k + v_k[c] beta_k)),
+//        alpha_k = v_k . v_j,  beta_k = w_k . v_j  (k = j0 .. j - 1);
+//     v_k[c] and w_k[c] at the workgroup's own columns are kept in LDS as they appear, and the
+//     dots are summed from per-workgroup partials over those same indices (all columns of all
+//     workgroups cover every row), published when v_j is formed at the end of step j - 1 and
+//     polled only after this step's column reads -- long arrived, so no second hop's latency;
+//   * the panel's first step (j = j0 > 0) flushes the previous panel: every column c > j gets its
+//     DF_NB updates A(r, c) -= sum_k v_k[r] w_k[c] + w_k[r] v_k[c] at once (waves split the rows,
+//     each row's 2 DF_NB panel values loaded once into registers for all the workgroup's columns),
+//     is written once and dotted with v_j;
+//   * the last steps (j >= jt, n - jt ~ DF_TAIL) update every column every step, as above.
+// Column bytes per step: 8 (n - j)^2 read, plus 16 (n - j)^2 per DF_NB steps for the flush.
+// Column j + 1 after step j is formed in LDS (over v_j, once read), w_j goes to Wv's column j.
+constexpr int DF_NB = 16;      // updates per panel (the flush: 2 DF_NB registers per row)
+constexpr int DF_TAIL = 1024;  // steps at the end with every update applied at once
+constexpr int DF_MAXP = 256;   // workgroups (the partials' poll: 16 per thread)
+
+__global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
+  extern __shared__ double lds[];
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  constexpr int PU = 8;  // (16 spills here: 8 row pairs per lane, 64 KB in flight per CU)
+  const int n = a.n, P = a.P, w = blockIdx.x, L = a.ldl, ncl = a.ncl;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double* red = lds + L;  // lds[0, n): v_j, then (the exchange) column j + 1 after step j
+  int* s_ok = reinterpret_cast<int*>(red + TRD_WAVES);
+  double* s_alpha = red + TRD_WAVES + 1;  // column j+1's entry j+2 after step j (dlarfg's alpha)
+  double* s_d = red + TRD_WAVES + 2;      // its entry j+1 (d_{j+1})
+  double* s_cl = red + TRD_WAVES + 3;     // its entry n-1 at the last step (e_{n-2})
+  double* vown = red + TRD_WAVES + 4;     // [DF_NB][ncl]: v_k at this workgroup's columns
+  double* wown = vown + DF_NB * ncl;      // [DF_NB][ncl]: w_k there
+  double* qraw = wown + DF_NB * ncl;      // [ncl]: later columns' A(:, c) . v_j
+  double* qpart = qraw + ncl;             // [TRD_WAVES][ncl]: the flush's per-wave dots
+  double* ab = qpart + TRD_WAVES * ncl;   // [2 DF_NB]: alpha_k, beta_k interleaved
+  const double* vcur = lds;
+  double tj;
+
+  {  // v_0 from column 0 (never updated: read in place, V's column 0 written by every workgroup)
+    double beta;
+    const int j = 0;
+    (void)j;
+    TRD_DELAY(0);
+    const double d0 = a.A[0];
+    tj = trd_reflector(n, 0, a.A, a.V, red, &beta);
+    for (int r = 1 + tid; r < n; r += TRD_THREADS) lds[r] = a.V[r];
+    __syncthreads();
+    if (w == 0 && tid == 0) {
+      a.d[0] = d0;
+      a.e[0] = beta;
+      a.tau[0] = tj;
+    }
+  }
+
+  for (int j = 0; j <= n - 3; ++j) {
+    const bool tail = j >= a.jt;
+    const int j0 = tail ? a.jt : j - j % DF_NB;  // this panel's first step
+    const int j1 = tail ? n - 1 : j0 + DF_NB;    // columns (j, j1]: updated every step
+    const int kk = j - j0;                       // updates pending on the later columns
+    const int r0 = (j + 1) & ~1;
+    const int i0 = (j + 1 - w + P - 1) / P;      // first own column > j: w + i0 P
+    const int id = (j1 + 1 - w + P - 1) / P;     // first own column > j1
+    const bool later = !tail && id < ncl && w + id * P < n;  // own columns past j1 (uniform)
+    const double* vprev = a.V + (size_t)(j > 0 ? j - 1 : 0) * a.lda;
+    const double* wprev = a.Wv + (size_t)(j > 0 ? j - 1 : 0) * a.lda;
+    double* pubcol = a.cpub + (size_t)(j + 1) * a.lda;
+    double sp = 0.0;  // this thread's share of p_j . v_j
+    TRD_STAMP(0);
+    TRD_WGSTAMP(0);
+    if (j == j0 && j > 0) {
+      // ---- flush: the previous panel's DF_NB updates on every own column c > j, then . v_j
+      for (int i = tid; i < TRD_WAVES * ncl; i += TRD_THREADS) qpart[i] = 0.0;
+      __syncthreads();
+      const int kb = j0 - DF_NB;
+      for (int rb = r0 + 64 * wv; rb < n; rb += 64 * TRD_WAVES) {
+        const int r = rb + lane;
+        const bool in = r < n;
+        double pv[DF_NB], pw[DF_NB];
+#pragma unroll
+        for (int q = 0; q < DF_NB; ++q) {
+          pv[q] = in ? a.V[(size_t)(kb + q) * a.lda + r] : 0.0;
+          pw[q] = in ? a.Wv[(size_t)(kb + q) * a.lda + r] : 0.0;
+        }
+        const double vr = in && r >= j + 1 ? vcur[r] : 0.0;
+        for (int ib = i0; ib < ncl; ib += 4) {  // (wave-uniform bounds)
+          double x[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int c = w + (ib + u) * P;
+            x[u] = in && ib + u < ncl && c < n ? a.A[(size_t)c * a.lda + r] : 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = ib + u, c = w + i * P;
+            if (i >= ncl || c >= n) break;
+#pragma unroll
+            for (int q = 0; q < DF_NB; ++q)
+              x[u] -= pv[q] * wown[q * ncl + i] + pw[q] * vown[q * ncl + i];
+            if (in) {
+              a.A[(size_t)c * a.lda + r] = x[u];
+              if (c == j + 1) st1(pubcol + r, x[u]);
+            }
+            const double sdot = wave_sum(x[u] * vr);
+            if (lane == 0) qpart[wv * ncl + i] += sdot;
+          }
+        }
+      }
+      __syncthreads();
+      for (int i = i0 + tid; i < ncl; i += TRD_THREADS) {
+        const int c = w + i * P;
+        if (c < n) {
+          double sdot = 0.0;
+#pragma unroll
+          for (int q = 0; q < TRD_WAVES; ++q) sdot += qpart[q * ncl + i];
+          const double p = tj * sdot;
+          st1(&a.pbuf[(size_t)j * a.lda + c], p);
+          sp += p * vcur[c];
+        }
+      }
+    } else {
+      // ---- the pass: one wave per own column c > j; (j, j1] read + updated (step j - 1) +
+      // written, later columns read only
+      for (int c = w + (i0 + wv) * P; c < n; c += TRD_WAVES * P) {
+        double* col = a.A + (size_t)c * a.lda;
+        const bool eager = c <= j1;
+        double dot = 0.0;
+        if (eager) {
+          const double wc = j > 0 ? wprev[c] : 0.0, vc = j > 0 ? vprev[c] : 0.0;
+          double* pub = c == j + 1 ? pubcol : nullptr;
+          for (int rb = r0 + 2 * lane; rb < n; rb += PU * 128) {
+            d2 x[PU];
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+              const int r = rb + 128 * u;
+              if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
+            }
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+              const int r = rb + 128 * u;
+              if (r < n) {
+                const d2 vv = *reinterpret_cast<const d2*>(vcur + r);
+                if (j > 0) {
+                  const d2 vp = *reinterpret_cast<const d2*>(vprev + r);
+                  const d2 wp = *reinterpret_cast<const d2*>(wprev + r);
+                  x[u].x -= vp.x * wc + wp.x * vc;
+                  x[u].y -= vp.y * wc + wp.y * vc;
+                  *reinterpret_cast<d2*>(col + r) = x[u];
+                }
+                if (pub) {
+                  st1(pub + r, x[u].x);
+                  st1(pub + r + 1, x[u].y);
+                }
+                if (c == n - 1 && j == n - 3) {  // A(n-1, n-1) for the last 2 x 2 block
+                  if (r == n - 1) st1(a.dlast, x[u].x);
+                  if (r + 1 == n - 1) st1(a.dlast, x[u].y);
+                }
+                dot += (r >= j + 1 ? x[u].x * vv.x : 0.0) + (r + 1 < n ? x[u].y * vv.y : 0.0);
+              }
+            }
+          }
+          const double p = tj * wave_sum(dot);
+          if (lane == 0) {
+            st1(&a.pbuf[(size_t)j * a.lda + c], p);
+            sp += p * vcur[c];
+          }
+        } else {
+          for (int rb = r0 + 2 * lane; rb < n; rb += PU * 128) {
+            d2 x[PU];
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+              const int r = rb + 128 * u;
+              if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
+            }
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+              const int r = rb + 128 * u;
+              if (r < n) {
+                const d2 vv = *reinterpret_cast<const d2*>(vcur + r);
+                dot += (r >= j + 1 ? x[u].x * vv.x : 0.0) + (r + 1 < n ? x[u].y * vv.y : 0.0);
+              }
+            }
+          }
+          const double sdot = wave_sum(dot);
+          if (lane == 0) qraw[(c - w) / P] = sdot;
+        }
+      }
+      __syncthreads();  // (qraw)
+      if (later && kk > 0) {
+        // alpha_k, beta_k: the P workgroups' partials of step j (published with v_j), 16
+        // threads per value, summed in a fixed order
+        TRD_DELAY(5);
+        constexpr int AK = DF_MAXP / 16;
+        const int q = tid >> 4, sub = tid & 15;
+        double v[AK];
+        const double* src[AK];
+#pragma unroll
+        for (int m = 0; m < AK; ++m) {
+          const int ww = sub + 16 * m;
+          const bool act = q < 2 * kk && ww < P;
+          src[m] = act ? &a.abuf[((size_t)j * 2 * DF_NB + q) * P + ww] : nullptr;
+          v[m] = act ? ld1(src[m]) : 0.0;
+        }
+        if (!trd_poll<AK>(a, n, j, s_ok, v, src)) return;
+        double sq = 0.0;
+#pragma unroll
+        for (int m = 0; m < AK; ++m) sq += v[m];
+        sq += __shfl_xor(sq, 1);
+        sq += __shfl_xor(sq, 2);
+        sq += __shfl_xor(sq, 4);
+        sq += __shfl_xor(sq, 8);
+        if (sub == 0 && q < 2 * kk) ab[q] = sq;
+        __syncthreads();
+      }
+      if (later) {
+        for (int i = id + tid; i < ncl; i += TRD_THREADS) {
+          const int c = w + i * P;
+          if (c < n) {
+            double sdot = qraw[i];
+            for (int k = 0; k < kk; ++k)
+              sdot -= wown[k * ncl + i] * ab[2 * k] + vown[k * ncl + i] * ab[2 * k + 1];
+            const double p = tj * sdot;
+            st1(&a.pbuf[(size_t)j * a.lda + c], p);
+            sp += p * vcur[c];
+          }
+        }
+      }
+    }
+    // ---- this step's entries of the panel: v_j at the own columns (w_j's: the exchange);
+    // (the flush and the corrections above read only earlier steps' entries, and the flush's
+    // reads of entry 0 precede its barrier)
+    if (!tail)
+      for (int i = tid; i < ncl; i += TRD_THREADS) {
+        const int c = w + i * P;
+        vown[kk * ncl + i] = c >= j + 1 && c < n ? vcur[c] : 0.0;
+        wown[kk * ncl + i] = 0.0;
+      }
+    // ---- publish this workgroup's part of p_j . v_j
+    TRD_STAMP(1);
+    TRD_DELAY(1);
+    const double spw = block_sum(sp, red);
+    TRD_WGSTAMP(1);
+    if (tid == 0) {
+#ifdef GPR_TESTING
+      if (!(j == a.fail_step && w == 0))
+#endif
+        st1(&a.parts[(size_t)j * P + w], spw);
+    }
+    // ---- Q^T B on the fly (as sytrd_kernel's GV variant)
+    if (a.m > w) {
+      const int mine = (a.m - w + P - 1) / P;
+      if (mine < 4) {
+        for (int c = w; c < a.m; c += P) {
+          double* b = a.B + (size_t)c * a.ldb;
+          double dot = 0.0;
+          for (int r = j + 1 + tid; r < n; r += TRD_THREADS) dot += b[r] * vcur[r];
+          const double f = tj * block_sum(dot, red);
+          for (int r = j + 1 + tid; r < n; r += TRD_THREADS) b[r] -= f * vcur[r];
+        }
+      } else {
+        for (int c = w + wv * P; c < a.m; c += TRD_WAVES * P) {
+          double* b = a.B + (size_t)c * a.ldb;
+          double dot = 0.0;
+          for (int rb = j + 1 + lane; rb < n; rb += 4 * 64) {
+            double x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = rb + 64 * u < n ? b[rb + 64 * u] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (rb + 64 * u < n) dot += x[u] * vcur[rb + 64 * u];
+          }
+          const double f = tj * wave_sum(dot);
+          for (int r = j + 1 + lane; r < n; r += 64) b[r] -= f * vcur[r];
+        }
+      }
+    }
+    __syncthreads();  // (every read of v_j in LDS above precedes the exchange's overwrite)
+    TRD_STAMP(2);
+    // ---- the exchange: p_j, the published column j + 1 and the P partial sums, polled (their
+    // sentinel is the arrival flag); w_j to Wv's column j, column j + 1 after step j over v_j in
+    // LDS (each row by the thread that read v_j there; row j + 1 and, at the last step, row n - 1
+    // to their own slots: v_j[j + 1] and v_j[n - 1] are still read after the loop)
+    double* wnew = a.Wv + (size_t)j * a.lda;
+    const double* pj = a.pbuf + (size_t)j * a.lda;
+    const double* pp = a.parts + (size_t)j * P;
+    TRD_DELAY(2);
+    double xn = 0.0;
+    {
+      double pv[2] = {ld1(&pj[j + 1]), tid < P ? ld1(&pp[tid]) : 0.0};
+      const double* ps[2] = {&pj[j + 1], tid < P ? &pp[tid] : nullptr};
+      if (!trd_poll<2>(a, n, j, s_ok, pv, ps)) return;
+      TRD_STAMP(3);
+      const double kj = 0.5 * tj * block_sum(pv[1], red);
+      TRD_STAMP(4);
+      const double wc = pv[0] - kj * vcur[j + 1], vc = vcur[j + 1];
+      for (int k0 = 0; j + 1 + k0 * TRD_THREADS < n; k0 += TRD_GCH) {  // (uniform bound)
+        double xv[2 * TRD_GCH];
+        const double* xs[2 * TRD_GCH];
+#pragma unroll
+        for (int k = 0; k < TRD_GCH; ++k) {
+          const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
+          xs[2 * k] = r < n ? &pj[r] : nullptr;
+          xs[2 * k + 1] = r < n ? &pubcol[r] : nullptr;
+          xv[2 * k] = r < n ? ld1(&pj[r]) : 0.0;
+          xv[2 * k + 1] = r < n ? ld1(&pubcol[r]) : 0.0;
+        }
+        if (!trd_poll<2 * TRD_GCH>(a, n, j, s_ok, xv, xs)) return;
+#pragma unroll
+        for (int k = 0; k < TRD_GCH; ++k) {
+          const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
+          if (r < n) {
+            const double wr = xv[2 * k] - kj * vcur[r];
+            const double x = xv[2 * k + 1] - (vcur[r] * wc + wr * vc);
+            wnew[r] = wr;
+            if (!tail && r >= w && (r - w) % P == 0) wown[kk * ncl + (r - w) / P] = wr;
+            if (r == j + 1) *s_d = x;
+            else if (j == n - 3 && r == n - 1) *s_cl = x;
+            else lds[r] = x;
+            if (r >= j + 3) xn += x * x;
+            if (r == j + 2) *s_alpha = x;
+          }
+        }
+      }
+    }
+    const double xnorm2 = block_sum(xn, red);  // (its barriers publish the LDS column, wnew)
+    const bool out = w == (j + 1) % P;         // (one workgroup writes T)
+    if (out && tid == 0) a.d[j + 1] = *s_d;
+    if (j + 1 <= n - 3) {
+      TRD_DELAY(3);
+      const double alpha = *s_alpha;
+      double tau = 0.0, beta = alpha, scal = 0.0;
+      if (xnorm2 > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
+        tau = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+      }
+      double* vj = a.V + (size_t)(j + 1) * a.lda;  // (every workgroup: the same bits)
+      for (int r = j + 2 + tid; r < n; r += TRD_THREADS) {
+        const double v = r == j + 2 ? 1.0 : lds[r] * scal;
+        vj[r] = v;
+        lds[r] = v;
+      }
+      if (out && tid == 0) {
+        a.e[j + 1] = beta;
+        a.tau[j + 1] = tau;
+      }
+      tj = tau;
+      TRD_DELAY(4);
+      __syncthreads();
+      // ---- the partials of alpha_k, beta_k for step j + 1 (inside a deferred panel): over the
+      // own columns, from LDS only
+      const int jn = j + 1, kn = jn % DF_NB;
+      if (jn < a.jt && kn != 0) {
+        TRD_DELAY(6);
+        for (int q = wv; q < 2 * kn; q += TRD_WAVES) {
+          const double* own = (q & 1) ? wown : vown;
+          double sq = 0.0;
+          for (int i = lane; i < ncl; i += 64) {
+            const int c = w + i * P;
+            if (c >= jn + 1 && c < n) sq += own[(q >> 1) * ncl + i] * lds[c];
+          }
+          sq = wave_sum(sq);
+          if (lane == 0) st1(&a.abuf[((size_t)jn * 2 * DF_NB + q) * P + w], sq);
+        }
+      }
+    } else if (out && tid == 0) {  // the last 2 x 2 block: e_{n-2}, d_{n-1}
+      a.e[n - 2] = *s_cl;
+      double dl = ld1(a.dlast);
+      for (long long spins = 0; trd_unset(dl) && spins <= a.spin_limit; ++spins) {
+        __builtin_amdgcn_s_sleep(1);
+        dl = ld1(a.dlast);
+      }
+      if (trd_unset(dl)) st1i(a.err, 1);
+      a.d[n - 1] = dl - 2.0 * vcur[n - 1] * wnew[n - 1];
+    }
+    TRD_STAMP(5);
   }
 }
 
@@ -775,13 +1168,21 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
                 double* dd, double* de) {
   if (n <= 0) return 0;
   if (n > TRD_MAXN_G) return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: n = %d > %d", n, TRD_MAXN_G);
-  const bool gv = n > TRD_MAXN;
   hipStream_t st = ctx->stream;
   if (ctx->ncu <= 0) {
     hipDeviceProp_t prop;
     HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
     ctx->ncu = prop.multiProcessorCount;
   }
+  // beyond TRD_MAXN: the deferred-update variant (DF) when its partials' poll covers the grid,
+  // else the per-step GV variant.  (Test build: GPR_TRD_DF = 0 the GV variant, 2 DF at any n --
+  // A/B and small-n parity; GPR_TRD_DF_TAIL the steps left to the tail.)
+  int df_mode = 1;
+  int df_tail = DF_TAIL;
+#ifdef GPR_TESTING
+  if (const char* e = getenv("GPR_TRD_DF")) df_mode = atoi(e);
+  if (const char* e = getenv("GPR_TRD_DF_TAIL")) df_tail = std::max(2 * DF_NB, atoi(e));
+#endif
   const size_t ld = (size_t)(n + 15) / 16 * 16;
   // workgroups: 8 columns each up to n ~ 1500, 16 above (profiles/r05_trd_sweep.txt: 4..24
   // columns change n = 512 / 1100 / 2048 / 4096 by <= 12 / 13 / 11 / 1 %), at most one per CU.
@@ -793,9 +1194,17 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 #ifdef GPR_TESTING
   if (const char* e = getenv("GPR_TRD_COLS")) cols = std::max(1, atoi(e));  // (tuning sweeps)
 #endif
-  const size_t shmem = ((gv ? 1 : 3) * (size_t)((n + 1) & ~1) + TRD_WAVES + 2) * sizeof(double);
-  const void* kfn = gv ? trd_kernel_ptr<16, RPT_G, true>()
-                       : n >= 800 ? trd_kernel_ptr<16, RPT, false>() : trd_kernel_ptr<8, RPT, false>();
+  const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
+  const int ncl = (n + P - 1) / P;
+  const bool df = P <= DF_MAXP && n >= 3 && ((n > TRD_MAXN && df_mode == 1) || df_mode == 2);
+  const bool gv = n > TRD_MAXN || df;
+  const size_t shmem =
+      df ? ((size_t)((n + 1) & ~1) + TRD_WAVES + 4 + (2 * DF_NB + 1 + TRD_WAVES) * (size_t)ncl + 2 * DF_NB) *
+               sizeof(double)
+         : ((gv ? 1 : 3) * (size_t)((n + 1) & ~1) + TRD_WAVES + 2) * sizeof(double);
+  const void* kfn = df   ? reinterpret_cast<const void*>(&sytrd_df_kernel)
+                    : gv ? trd_kernel_ptr<16, RPT_G, true>()
+                         : n >= 800 ? trd_kernel_ptr<16, RPT, false>() : trd_kernel_ptr<8, RPT, false>();
   // co-residency: one workgroup per CU (the launch bound and, for the LDS variant, its vectors
   // allow no more); none at all is refused here, and the cooperative launch below refuses a grid
   // that cannot be resident as a whole
@@ -805,8 +1214,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
     (void)hipGetLastError();
     return set_err(ctx, GPR_E_UNSUP, "tridiagonal reduction: no resident workgroup possible");
   }
-  const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
-  // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), tau, dlast, then ints
+  // workspace: W, V, cpub, pbuf (ld x n each), parts (n x P), (DF) abuf, tau, dlast, then ints
   const size_t nW = ld * n;
   const size_t nI = (size_t)n + 2;  // counters, err (as doubles: half of it, rounded up)
   const int n2 = (int)ld;
@@ -821,15 +1229,18 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
                         ? 2 * (size_t)n2 * QB + 2 * (size_t)QB * QB + 2 * (size_t)QB * m +
                               (size_t)gw_S * QB * (QB + m)
                         : 0;
-  const size_t nG = gv ? 8 * ld : 0;  // (GV: the w and column-(j+1) rings, 4 columns each)
-  const size_t need = 4 * nW + (size_t)n * P + (size_t)n + 8 + nI + nQ + nG;
+  // (GV: the w and column-(j+1) rings, 4 columns each; DF: Wv, ld x n)
+  const size_t nG = df ? nW : gv ? 8 * ld : 0;
+  const size_t nA = df ? (size_t)n * 2 * DF_NB * P : 0;  // (DF: the panel's dot partials)
+  const size_t need = 4 * nW + (size_t)n * P + nA + (size_t)n + 8 + nI + nQ + nG;
   GPR_TRY(ensure_buf(ctx, &ctx->deig, &ctx->eig_cap, need));
   double* W = ctx->deig;
   double* V = W + nW;
   double* cpub = V + nW;
   double* pbuf = cpub + nW;
   double* parts = pbuf + nW;
-  double* tau = parts + (size_t)n * P;
+  double* abuf = parts + (size_t)n * P;
+  double* tau = abuf + nA;
   double* dlast = tau + n;
   int* ints = reinterpret_cast<int*>(dlast + 8);
   int* err = ints + n;
@@ -845,8 +1256,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   trd_copy_kernel<<<1024, 256, 0, st>>>(dA, (size_t)lda, n, W, ld);
   LAUNCH_CHECK(ctx);
   HIP_TRY(ctx, hipMemsetAsync(ints, 0, sizeof(int) * ((size_t)n + 2), st));
-  // cpub, pbuf, parts (contiguous) and dlast start "unset" (the exchange polls on the values)
-  trd_fill_unset_kernel<<<1024, 256, 0, st>>>(cpub, 2 * nW + (size_t)n * P);
+  // cpub, pbuf, parts, abuf (contiguous) and dlast start "unset" (the exchange polls on the values)
+  trd_fill_unset_kernel<<<1024, 256, 0, st>>>(cpub, 2 * nW + (size_t)n * P + nA);
   trd_fill_unset_kernel<<<1, 64, 0, st>>>(dlast, 1);
   LAUNCH_CHECK(ctx);
   HIP_TRY(ctx, hipMemsetAsync(tau, 0, sizeof(double) * n, st));
@@ -876,8 +1287,16 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;
   a.m = fused_b ? m : 0;
-  a.wr = gv ? rings : nullptr;
-  a.xr = gv ? rings + 4 * ld : nullptr;
+  a.wr = gv && !df ? rings : nullptr;
+  a.xr = gv && !df ? rings + 4 * ld : nullptr;
+  a.Wv = df ? rings : nullptr;
+  a.abuf = df ? abuf : nullptr;
+  a.jt = df ? std::max(0, (n - df_tail) / DF_NB * DF_NB) : 0;
+  a.ncl = ncl;
+  a.nt = 0;
+#ifdef GPR_TESTING
+  if (const char* e = getenv("GPR_TRD_NT")) a.nt = atoi(e);  // (A/B)
+#endif
   // cooperative: all P workgroups resident together, or the runtime refuses the launch (nothing
   // has run then: B is untouched, and the caller falls back)
   void* kargs[] = {&a};
@@ -969,7 +1388,8 @@ extern "C" int gpr_testing_trd_wg_trace(long long* out) {
 }
 
 extern "C" int gpr_testing_trd_trace(long long* out, int n) {
-  if (n < 1 || n > TRD_MAXN) return GPR_E_ARG;
+  if (n < 1) return GPR_E_ARG;
+  n = std::min(n, TRD_MAXN);  // (the first TRD_MAXN steps are stamped)
   std::vector<long long> h(2 * (size_t)TRD_MAXN * 6);
   if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_trd_trace), h.size() * sizeof(long long)) != hipSuccess)
     return GPR_E_HIP;

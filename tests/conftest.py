@@ -61,7 +61,8 @@ def run_fault_scenario(name, *args, timeout=300):
     assert os.path.exists(TESTING_LIB), "build it: make -C gaussianprocessregression.jl_amd/csrc"
     env = dict(os.environ, GPR_HIP_LIB=TESTING_LIB)
     for k in ("GPR_DAG_SPIN_LIMIT", "GPR_MGPU_GATE_LIMIT", "GPR_MGPU_FAIL_UNPACK",
-              "GPR_TRD_FAIL_STEP", "GPR_TRD_SPIN_LIMIT", "GPR_TRD_QCHUNK"):
+              "GPR_TRD_FAIL_STEP", "GPR_TRD_SPIN_LIMIT", "GPR_TRD_QCHUNK",
+              "GPR_TRD_DF", "GPR_TRD_DF_TAIL", "GPR_TRD_DELAY"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "fault_scenarios.py"), name,
                         *map(str, args)], env=env, cwd=ROOT, capture_output=True, text=True,

@@ -5,7 +5,8 @@ never make it time out or drop a chunk on purpose; these scenarios need the swit
 build reads at call time: GPR_DAG_SPIN_LIMIT (every tile-DAG dependency wait gives up at once),
 GPR_MGPU_GATE_LIMIT (a streamed broadcast chunk's gate gives up), GPR_MGPU_FAIL_UNPACK (a
 receiver's unpack of chunk k fails), GPR_TRD_FAIL_STEP / GPR_TRD_SPIN_LIMIT (a tridiagonal
-reduction hand-off that never completes), GPR_TRD_QCHUNK (the quadrature's tridiagonal solves
+reduction hand-off that never completes), GPR_TRD_DF / GPR_TRD_DF_TAIL (the deferred-update
+reduction at small n), GPR_TRD_QCHUNK (the quadrature's tridiagonal solves
 in launches of a few columns), GPR_MGPU_SELF_BCAST (a one-device handle broadcasting to itself)
 and the rocSOLVER eigen comparator (GPR_QUAD_EIGEN=2).
 
@@ -98,6 +99,60 @@ def trd_timeout():
     T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
     nrm = np.linalg.norm(A, 2)
     assert np.max(np.abs(np.linalg.eigvalsh(T) - np.linalg.eigvalsh(A))) <= 4 * n * np.finfo(float).eps * nrm
+
+
+def trd_df_small():
+    """The large-n reduction's deferred-update variant (tridiag.hip sytrd_df_kernel: panels of
+    16 steps whose later columns are only read and corrected, flushed at each panel's start)
+    forced at small n in the test build (GPR_TRD_DF=2, GPR_TRD_DF_TAIL=64: every panel but the
+    last 64 steps deferred), so its panel / flush / tail boundaries, odd n and grids of 13-256
+    workgroups run in seconds: eigenvalues of T within 4 n eps ||A|| of numpy's, ||Q^T B||
+    preserved and B^T (A + s I)^{-1} B through T against numpy; once more with late-wave
+    injection (GPR_TRD_DELAY=1); and a hand-off that never completes times out cleanly."""
+    import scipy.linalg as sla
+    import gpr_amd as G
+    ctx = G.Context(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    os.environ["GPR_TRD_DF"] = "2"
+    os.environ["GPR_TRD_DF_TAIL"] = "64"
+    eps = np.finfo(float).eps
+    for n, delay in ((100, 0), (701, 0), (2051, 0), (4100, 0), (701, 1)):
+        os.environ["GPR_TRD_DELAY"] = str(delay)
+        rng = np.random.default_rng(n)
+        X = rng.standard_normal((n, n))
+        A = (X + X.T) / 2
+        B = rng.standard_normal((n, 3))
+        dA, dB = ctx.colmajor(A), ctx.colmajor(B)
+        dd, de = ctx.empty(n), ctx.empty(n)
+        assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, n, P(dB), 3, n, P(dd), P(de)) == 0, \
+            G._lib.lib.gpr_last_error(ctx.h)
+        d, e, C = ctx.host(dd)[:n], ctx.host(de)[:n - 1], ctx.host(dB)[:n]
+        T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+        nrm = np.linalg.norm(A, 2)
+        lam = np.linalg.eigvalsh(A)
+        err = np.max(np.abs(np.linalg.eigvalsh(T) - lam))
+        assert err <= 4 * n * eps * nrm, (n, delay, err)
+        np.testing.assert_allclose(np.linalg.norm(C, axis=0), np.linalg.norm(B, axis=0), rtol=1e-12)
+        s = 0.5 * nrm + 0.1  # (A + s I: indefinite, away from singular)
+        want = B.T @ np.linalg.solve(A + s * np.eye(n), B)
+        got = C.T @ sla.solve_banded((1, 1), np.vstack([np.r_[0.0, e], d + s, np.r_[e, 0.0]]), C)
+        cond = np.max(np.abs(lam + s)) / np.min(np.abs(lam + s))
+        np.testing.assert_allclose(got, want, rtol=1e-11 * cond, atol=1e-11 * cond * np.abs(want).max())
+    os.environ["GPR_TRD_DELAY"] = "0"
+    # a partial sum of step 21 (a deferred panel's 6th step) never published: every workgroup
+    # gives up, the call reports it, and the same context reduces correctly afterwards
+    n = 701
+    A = np.random.default_rng(5).standard_normal((n, n))
+    A = (A + A.T) / 2
+    dA, dd, de = ctx.colmajor(A), ctx.empty(n), ctx.empty(n)
+    call = lambda: G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, n, None, 0, n, P(dd), P(de))  # noqa: E731
+    os.environ["GPR_TRD_FAIL_STEP"] = "21"
+    os.environ["GPR_TRD_SPIN_LIMIT"] = "4096"
+    assert call() == -2 and b"timed out" in G._lib.lib.gpr_last_error(ctx.h)
+    del os.environ["GPR_TRD_FAIL_STEP"], os.environ["GPR_TRD_SPIN_LIMIT"]
+    assert call() == 0
+    T = np.diag(ctx.host(dd)[:n]) + np.diag(ctx.host(de)[:n - 1], 1) + np.diag(ctx.host(de)[:n - 1], -1)
+    assert np.max(np.abs(np.linalg.eigvalsh(T) - np.linalg.eigvalsh(A))) <= 4 * n * eps * np.linalg.norm(A, 2)
 
 
 def trd_quad_chunks():

@@ -274,6 +274,15 @@ def test_sytrd_handoff_timeout_drains_and_context_recovers():
     run_fault_scenario("trd_timeout")
 
 
+def test_sytrd_deferred_updates_small_n():
+    """The deferred-update reduction (n > 6144 by default) forced at n = 100 .. 4100 in the test
+    build, with every panel but the last 64 steps deferred: eigenvalues, Q^T B norms and a
+    shifted quadratic form against numpy, once under late-wave injection, and a hand-off
+    time-out inside a deferred panel (tests/fault_scenarios.py trd_df_small)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("trd_df_small", timeout=600)
+
+
 @pytest.mark.parametrize("n", [6144, 8192, 8200])
 def test_syev_large_known_spectrum(n):
     """Large sizes with a known spectrum: n = 6144, the LDS variants' largest (three n-vectors

@@ -102,10 +102,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 __device__ long long g_trd_trace[2][TRD_MAXN][6];
 // every workgroup's pass start / pass end at every 64th step (the spread across workgroups)
 __device__ long long g_trd_wg[TRD_MAXN / 64][256][2];
-#define TRD_WGSTAMP(k)                                                             \
-  do {                                                                             \
-    if (tid == 0 && (j & 63) == 0 && w < 256 && j < TRD_MAXN)                      \
-      g_trd_wg[j >> 6][w][k] = (long long)__builtin_amdgcn_s_memrealtime();        \
+#define TRD_WGSTAMP(k)                                                                      \
+  do {                                                                                      \
+    if (tid == 0 && j >= a.wgoff && ((j - a.wgoff) & 63) == 0 && w < 256 && j < TRD_MAXN)  \
+      g_trd_wg[(j - a.wgoff) >> 6][w][k] = (long long)__builtin_amdgcn_s_memrealtime();     \
   } while (0)
 #define TRD_STAMP(k)                                                                   \
   do {                                                                                 \
@@ -138,6 +138,7 @@ struct TrdArgs {
 #ifdef GPR_TESTING
   int fail_step;    // (test build) workgroup 0 never publishes its partial sum of this step
   int delay;        // (test build) GPR_TRD_DELAY: late-wave injection, see trd_delay
+  int wgoff;        // (test build) GPR_TRD_WGOFF: the per-workgroup stamps at steps wgoff + 64 k
 #endif
   double* B;        // optional n x m (ld ldb): B <- H_j B at step j (column c to workgroup c mod P)
   size_t ldb;
@@ -676,11 +677,55 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
         }
       }
     } else {
-      // ---- the pass: one wave per own column c > j; (j, j1] read + updated (step j - 1) +
-      // written, later columns read only
-      for (int c = w + (i0 + wv) * P; c < n; c += TRD_WAVES * P) {
+      // ---- the pass.  A deferred panel's own columns in (j, j1] (one at most for P >= DF_NB):
+      // the whole workgroup on each, rows split over the threads -- read, updated (step j - 1),
+      // written (one wave per such column made its workgroup the step's straggler: ~1.6x the
+      // pass, profiles/r06_trd_wg_df.txt)
+      if (!tail)
+        for (int i = i0; i < ncl; ++i) {
+          const int c = w + i * P;
+          if (c > j1 || c >= n) break;  // (uniform)
+          double* col = a.A + (size_t)c * a.lda;
+          const double wc = j > 0 ? wprev[c] : 0.0, vc = j > 0 ? vprev[c] : 0.0;
+          double dot = 0.0;
+          for (int rb = r0 + 2 * tid; rb < n; rb += 8 * TRD_THREADS) {
+            d2 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int r = rb + 2 * TRD_THREADS * u;
+              if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int r = rb + 2 * TRD_THREADS * u;
+              if (r < n) {
+                const d2 vv = *reinterpret_cast<const d2*>(vcur + r);
+                if (j > 0) {
+                  const d2 vp = *reinterpret_cast<const d2*>(vprev + r);
+                  const d2 wp = *reinterpret_cast<const d2*>(wprev + r);
+                  x[u].x -= vp.x * wc + wp.x * vc;
+                  x[u].y -= vp.y * wc + wp.y * vc;
+                  *reinterpret_cast<d2*>(col + r) = x[u];
+                }
+                if (c == j + 1) {
+                  st1(pubcol + r, x[u].x);
+                  st1(pubcol + r + 1, x[u].y);
+                }
+                dot += (r >= j + 1 ? x[u].x * vv.x : 0.0) + (r + 1 < n ? x[u].y * vv.y : 0.0);
+              }
+            }
+          }
+          const double p = tj * block_sum(dot, red);
+          if (tid == 0) {
+            st1(&a.pbuf[(size_t)j * a.lda + c], p);
+            sp += p * vcur[c];
+          }
+        }
+      // one wave per own column: the tail's (every column read + updated + written), or a
+      // deferred panel's columns past j1 (read only)
+      for (int c = w + ((tail ? i0 : id) + wv) * P; c < n; c += TRD_WAVES * P) {
         double* col = a.A + (size_t)c * a.lda;
-        const bool eager = c <= j1;
+        const bool eager = tail;
         double dot = 0.0;
         if (eager) {
           const double wc = j > 0 ? wprev[c] : 0.0, vc = j > 0 ? vprev[c] : 0.0;
@@ -1283,6 +1328,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.fail_step = getenv("GPR_TRD_FAIL_STEP") ? atoi(getenv("GPR_TRD_FAIL_STEP")) : -1;
   if (const char* e = getenv("GPR_TRD_SPIN_LIMIT")) a.spin_limit = atoll(e);
   a.delay = getenv("GPR_TRD_DELAY") ? std::max(0, atoi(getenv("GPR_TRD_DELAY"))) : 0;
+  a.wgoff = getenv("GPR_TRD_WGOFF") ? std::max(0, std::min(63, atoi(getenv("GPR_TRD_WGOFF")))) : 0;
 #endif
   a.B = fused_b ? dB : nullptr;
   a.ldb = (size_t)ldb;

@@ -1,5 +1,5 @@
 """Per-workgroup pass times of the tridiagonal reduction (test build libgpr_hip_testing.so,
-GPR_HIP_LIB): at steps 0, 64, 128, ... every workgroup's pass duration and pass-end time
+GPR_HIP_LIB): at steps o, o + 64, o + 128, ... (o: GPR_TRD_WGOFF, default 0) every workgroup's pass duration and pass-end time
 relative to the earliest, summarised per XCD (workgroup w runs on XCD w mod 8)."""
 import ctypes
 import os
@@ -30,7 +30,7 @@ def main():
     tr = np.zeros((6144 // 64, 256, 2), dtype=np.int64)
     assert lib.gpr_testing_trd_wg_trace(tr.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong))) == 0
     nwg = min(256, (n + 15) // 16) if n > 1536 else min(256, (n + 7) // 8)
-    for s in range(0, (n - 2) // 64):
+    for s in range(0, min((n - 2) // 64, 6144 // 64)):  # (steps stamped: below TRD_MAXN)
         st = tr[s, :nwg].astype(np.float64) * 0.01  # us
         dur = st[:, 1] - st[:, 0]
         end = st[:, 1] - st[:, 1].min()
@@ -40,6 +40,9 @@ def main():
             print(f"step {64 * s:5d}: pass {dur.mean():6.2f} us (min {dur.min():6.2f} max {dur.max():6.2f}); "
                   f"start spread {start.max():5.2f}; end spread {end.max():6.2f} us; "
                   f"mean end by XCD " + " ".join(f"{v:5.2f}" for v in byx), flush=True)
+            slow = np.argsort(-dur)[:6]
+            print("      slowest: " + " ".join(f"w{w}:{dur[w]:.1f}" for w in slow) +
+                  f"  (median {np.median(dur):.1f})", flush=True)
 
 
 if __name__ == "__main__":

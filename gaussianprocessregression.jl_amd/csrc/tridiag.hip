@@ -566,15 +566,15 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
 //     workgroups cover every row), published when v_j is formed at the end of step j - 1 and
 //     polled only after this step's column reads -- long arrived, so no second hop's latency;
 //   * the panel's first step (j = j0 > 0) flushes the previous panel: every column c > j gets its
-//     DF_NB updates A(r, c) -= sum_k v_k[r] w_k[c] + w_k[r] v_k[c] at once (waves split the rows,
-//     each row's 2 DF_NB panel values loaded once into registers for all the workgroup's columns),
-//     is written once and dotted with v_j;
+//     DF_NB updates A(r, c) -= sum_k v_k[r] w_k[c] + w_k[r] v_k[c] at once (a K = 2 DF_NB GEMM on
+//     the FP64 MFMA, waves splitting the rows), is written once and dotted with v_j;
 //   * the last steps (j >= jt, n - jt ~ DF_TAIL) update every column every step, as above.
 // Column bytes per step: 8 (n - j)^2 read, plus 16 (n - j)^2 per DF_NB steps for the flush.
 // Column j + 1 after step j is formed in LDS (over v_j, once read), w_j goes to Wv's column j.
 constexpr int DF_NB = 16;      // updates per panel (the flush: 2 DF_NB registers per row)
 constexpr int DF_TAIL = 1024;  // steps at the end with every update applied at once
 constexpr int DF_MAXP = 256;   // workgroups (the partials' poll: 16 per thread)
+constexpr int DF_MAXCT = 4;    // the flush's column tiles of 16: ncl <= 64 (n <= 16384 at P = 256)
 
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
   extern __shared__ double lds[];
@@ -627,43 +627,80 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
     TRD_STAMP(0);
     TRD_WGSTAMP(0);
     if (j == j0 && j > 0) {
-      // ---- flush: the previous panel's DF_NB updates on every own column c > j, then . v_j
-      for (int i = tid; i < TRD_WAVES * ncl; i += TRD_THREADS) qpart[i] = 0.0;
-      __syncthreads();
+      // ---- flush: the previous panel's DF_NB updates on every own column c > j, then . v_j.
+      // A GEMM, X(rows, own columns) -= [V W](rows, 2 DF_NB) [w_k[c]; v_k[c]](2 DF_NB, columns),
+      // on the FP64 MFMA 16x16x4: first operand the coefficients (lane l: column l & 15 of the
+      // column tile, k = l >> 4 of the k-step), second the panel rows (row l & 15), so the result
+      // in lane l, entry q is (column (l >> 4) + 4 q, row l & 15): every load and store of X one
+      // 128-B column segment per 16 lanes.  Waves split the 16-row tiles, each tile's 2 DF_NB
+      // panel values loaded once for all column tiles.  (The same update as VALU FMAs with the
+      // coefficients read from LDS per element took ~5x the flush's own HBM time.)
       const int kb = j0 - DF_NB;
-      for (int rb = r0 + 64 * wv; rb < n; rb += 64 * TRD_WAVES) {
-        const int r = rb + lane;
-        const bool in = r < n;
-        double pv[DF_NB], pw[DF_NB];
+      const int nct = (ncl - i0 + 15) / 16;  // column tiles of the own columns > j (<= DF_MAXCT)
+      const int lr = lane & 15, lg = lane >> 4;
+      typedef double d4 __attribute__((ext_vector_type(4)));
+      double dacc[DF_MAXCT][4];
 #pragma unroll
-        for (int q = 0; q < DF_NB; ++q) {
-          pv[q] = in ? a.V[(size_t)(kb + q) * a.lda + r] : 0.0;
-          pw[q] = in ? a.Wv[(size_t)(kb + q) * a.lda + r] : 0.0;
+      for (int ct = 0; ct < DF_MAXCT; ++ct)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dacc[ct][q] = 0.0;
+      for (int rt = r0 + 16 * wv; rt < n; rt += 16 * TRD_WAVES) {
+        const int r = rt + lr;
+        const bool rin = r < n;
+        double bv[4], bw[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const size_t k = kb + lg + 4 * s4;
+          bv[s4] = rin ? a.V[k * a.lda + r] : 0.0;
+          bw[s4] = rin ? a.Wv[k * a.lda + r] : 0.0;
         }
-        const double vr = in && r >= j + 1 ? vcur[r] : 0.0;
-        for (int ib = i0; ib < ncl; ib += 4) {  // (wave-uniform bounds)
-          double x[4];
+        const double vr = rin && r >= j + 1 ? vcur[r] : 0.0;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int c = w + (ib + u) * P;
-            x[u] = in && ib + u < ncl && c < n ? a.A[(size_t)c * a.lda + r] : 0.0;
+        for (int ct = 0; ct < DF_MAXCT; ++ct) {
+          if (ct >= nct) break;  // (uniform)
+          d4 acc;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = i0 + 16 * ct + lg + 4 * q, c = w + i * P;
+            acc[q] = rin && i < ncl && c < n ? a.A[(size_t)c * a.lda + r] : 0.0;
+          }
+          const int ia = i0 + 16 * ct + lr;
+          const bool cin = ia < ncl && w + ia * P < n;
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int k = lg + 4 * s4;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cin ? -wown[k * ncl + ia] : 0.0, bv[s4], acc, 0, 0, 0);
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = ib + u, c = w + i * P;
-            if (i >= ncl || c >= n) break;
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int k = lg + 4 * s4;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cin ? -vown[k * ncl + ia] : 0.0, bw[s4], acc, 0, 0, 0);
+          }
 #pragma unroll
-            for (int q = 0; q < DF_NB; ++q)
-              x[u] -= pv[q] * wown[q * ncl + i] + pw[q] * vown[q * ncl + i];
-            if (in) {
-              a.A[(size_t)c * a.lda + r] = x[u];
-              if (c == j + 1) st1(pubcol + r, x[u]);
+          for (int q = 0; q < 4; ++q) {
+            const int i = i0 + 16 * ct + lg + 4 * q, c = w + i * P;
+            if (rin && i < ncl && c < n) {
+              a.A[(size_t)c * a.lda + r] = acc[q];
+              if (c == j + 1) st1(pubcol + r, acc[q]);
             }
-            const double sdot = wave_sum(x[u] * vr);
-            if (lane == 0) qpart[wv * ncl + i] += sdot;
+            dacc[ct][q] += acc[q] * vr;
           }
         }
       }
+      // per column: the sum over this wave's rows (lanes l & 15, fixed order), one writer per
+      // (wave, column)
+#pragma unroll
+      for (int ct = 0; ct < DF_MAXCT; ++ct)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double sq = dacc[ct][q];
+          sq += __shfl_xor(sq, 1);
+          sq += __shfl_xor(sq, 2);
+          sq += __shfl_xor(sq, 4);
+          sq += __shfl_xor(sq, 8);
+          const int i = i0 + 16 * ct + lg + 4 * q;
+          if (ct < nct && lr == 0 && i < ncl) qpart[wv * ncl + i] = sq;
+        }
       __syncthreads();
       for (int i = i0 + tid; i < ncl; i += TRD_THREADS) {
         const int c = w + i * P;
@@ -1241,7 +1278,7 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 #endif
   const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
   const int ncl = (n + P - 1) / P;
-  const bool df = P <= DF_MAXP && n >= 3 && ((n > TRD_MAXN && df_mode == 1) || df_mode == 2);
+  const bool df = P <= DF_MAXP && ncl <= 16 * DF_MAXCT && n >= 3 && ((n > TRD_MAXN && df_mode == 1) || df_mode == 2);
   const bool gv = n > TRD_MAXN || df;
   const size_t shmem =
       df ? ((size_t)((n + 1) & ~1) + TRD_WAVES + 4 + (2 * DF_NB + 1 + TRD_WAVES) * (size_t)ncl + 2 * DF_NB) *

@@ -574,7 +574,11 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
 constexpr int DF_NB = 16;      // updates per panel (the flush: 2 DF_NB registers per row)
 constexpr int DF_TAIL = 1024;  // steps at the end with every update applied at once
 constexpr int DF_MAXP = 256;   // workgroups (the partials' poll: 16 per thread)
-constexpr int DF_MAXCT = 4;    // the flush's column tiles of 16: ncl <= 64 (n <= 16384 at P = 256)
+constexpr int DF_MAXCT = 4;
+// DF from here on: faster than the LDS variant from n ~ 4600 (profiles/r06_trd_df_vs_lds.txt:
+// 5120 155.5 vs 166.1 ms, 6144 227.9 vs 259.8; 4096 101.5 vs 94.8, 3072 62.5 vs 43.4 -- below,
+// the work copy stays in the Infinity Cache and the per-step passes are cheap)
+constexpr int TRD_DF_MIN = 4608;    // the flush's column tiles of 16: ncl <= 64 (n <= 16384 at P = 256)
 
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
   extern __shared__ double lds[];
@@ -1256,8 +1260,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
     HIP_TRY(ctx, hipGetDeviceProperties(&prop, ctx->device));
     ctx->ncu = prop.multiProcessorCount;
   }
-  // beyond TRD_MAXN: the deferred-update variant (DF) when its partials' poll covers the grid,
-  // else the per-step GV variant.  (Test build: GPR_TRD_DF = 0 the GV variant, 2 DF at any n --
+  // from TRD_DF_MIN on: the deferred-update variant (DF) when its partials' poll and flush tiles
+  // cover the grid, else (beyond TRD_MAXN) the per-step GV variant.  (Test build: GPR_TRD_DF = 0 the GV variant, 2 DF at any n --
   // A/B and small-n parity; GPR_TRD_DF_TAIL the steps left to the tail.)
   int df_mode = 1;
   int df_tail = DF_TAIL;
@@ -1278,7 +1282,8 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
 #endif
   const int P = std::max(1, std::min(std::min(ctx->ncu, TRD_THREADS), (n + cols - 1) / cols));
   const int ncl = (n + P - 1) / P;
-  const bool df = P <= DF_MAXP && ncl <= 16 * DF_MAXCT && n >= 3 && ((n > TRD_MAXN && df_mode == 1) || df_mode == 2);
+  const bool df = P <= DF_MAXP && ncl <= 16 * DF_MAXCT && n >= 3 &&
+                  ((n >= TRD_DF_MIN && df_mode == 1) || df_mode == 2);
   const bool gv = n > TRD_MAXN || df;
   const size_t shmem =
       df ? ((size_t)((n + 1) & ~1) + TRD_WAVES + 4 + (2 * DF_NB + 1 + TRD_WAVES) * (size_t)ncl + 2 * DF_NB) *

@@ -275,7 +275,7 @@ def test_sytrd_handoff_timeout_drains_and_context_recovers():
 
 
 def test_sytrd_deferred_updates_small_n():
-    """The deferred-update reduction (n > 6144 by default) forced at n = 100 .. 4100 in the test
+    """The deferred-update reduction (n >= 4608 by default) forced at n = 100 .. 4100 in the test
     build, with every panel but the last 64 steps deferred: eigenvalues, Q^T B norms and a
     shifted quadratic form against numpy, once under late-wave injection, and a hand-off
     time-out inside a deferred panel (tests/fault_scenarios.py trd_df_small)."""
@@ -283,12 +283,12 @@ def test_sytrd_deferred_updates_small_n():
     run_fault_scenario("trd_df_small", timeout=600)
 
 
-@pytest.mark.parametrize("n", [6144, 8192, 8200])
+@pytest.mark.parametrize("n", [4100, 6144, 8192, 8200, 16384])
 def test_syev_large_known_spectrum(n):
-    """Large sizes with a known spectrum: n = 6144, the LDS variants' largest (three n-vectors
-    of LDS per reduction workgroup; the merge sort in LDS); 8192, the reduction's global-vector
-    variant (its vectors beyond LDS) with the top merge still sorted in LDS; 8200, the top merge
-    sorted in global memory.  A = H3 H2 H1 diag(ev) H1 H2 H3 with Householder H_k, so the
+    """Large sizes with a known spectrum: n = 4100, the LDS variant's reduction; 6144 and up its
+    deferred-update variant (DF) with the merge sort in LDS; 8200, the top merge sorted in global
+    memory; 16384, both bounds (DF's largest LDS footprint: 64 columns per workgroup).
+    A = H3 H2 H1 diag(ev) H1 H2 H3 with Householder H_k, so the
     eigenvalues are ev exactly; eigenvalues within 4 n eps ||A||, column norms of P^T B
     preserved, and the quadratic form B^T (A + s I)^{-1} B from the eigenpairs against the same
     form from the known factors."""

@@ -107,6 +107,13 @@ __device__ long long g_trd_wg[TRD_MAXN / 64][256][2];
     if (tid == 0 && j >= a.wgoff && ((j - a.wgoff) & 63) == 0 && w < 256 && j < TRD_MAXN)  \
       g_trd_wg[(j - a.wgoff) >> 6][w][k] = (long long)__builtin_amdgcn_s_memrealtime();     \
   } while (0)
+// (DF's exchange phase split: after the row chunks, after the reflector -- [2][TRD_MAXN][2])
+__device__ long long g_trd_trace2[2][TRD_MAXN][2];
+#define TRD_STAMP2(k)                                                                   \
+  do {                                                                                  \
+    if (tid == 0 && (w == 0 || w == P - 1) && j < TRD_MAXN)                             \
+      g_trd_trace2[w == 0 ? 0 : 1][j][k] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define TRD_STAMP(k)                                                                   \
   do {                                                                                 \
     if (tid == 0 && (w == 0 || w == P - 1) && j < TRD_MAXN)                            \
@@ -118,6 +125,9 @@ __device__ long long g_trd_wg[TRD_MAXN / 64][256][2];
   } while (0)
 #define TRD_WGSTAMP(k) \
   do {                 \
+  } while (0)
+#define TRD_STAMP2(k) \
+  do {                \
   } while (0)
 #endif
 
@@ -965,6 +975,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
         }
       }
     }
+    TRD_STAMP2(0);
     const double xnorm2 = block_sum(xn, red);  // (its barriers publish the LDS column, wnew)
     const bool out = w == (j + 1) % P;         // (one workgroup writes T)
     if (out && tid == 0) a.d[j + 1] = *s_d;
@@ -992,6 +1003,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
       __syncthreads();
       // ---- the partials of alpha_k, beta_k for step j + 1 (inside a deferred panel): over the
       // own columns, from LDS only
+      TRD_STAMP2(1);
       const int jn = j + 1, kn = jn % DF_NB;
       if (jn < a.jt && kn != 0) {
         TRD_DELAY(6);
@@ -1472,6 +1484,18 @@ extern "C" int gpr_testing_trd_wg_trace(long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trd_wg), sizeof(long long) * (TRD_MAXN / 64) * 256 * 2) !=
       hipSuccess)
     return GPR_E_HIP;
+  return 0;
+}
+
+extern "C" int gpr_testing_trd_trace2(long long* out, int n) {
+  if (n < 1) return GPR_E_ARG;
+  n = std::min(n, TRD_MAXN);
+  std::vector<long long> h(2 * (size_t)TRD_MAXN * 2);
+  if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_trd_trace2), h.size() * sizeof(long long)) != hipSuccess)
+    return GPR_E_HIP;
+  for (int k = 0; k < 2; ++k)
+    std::copy(h.begin() + (size_t)k * TRD_MAXN * 2, h.begin() + ((size_t)k * TRD_MAXN + n) * 2,
+              out + (size_t)k * n * 2);
   return 0;
 }
 

@@ -37,11 +37,21 @@ def main():
             nxt = t[1:, 0] - t[:-1, 5]
             total = (t[-1, 5] - t[0, 0])
             print(f"n={n} {who}: total {total / 1e3:.2f} ms over {st} steps ({total / st:.2f} us/step)")
+            t2 = None
+            if hasattr(lib, "gpr_testing_trd_trace2"):  # (DF: the exchange phase split)
+                tr2 = np.zeros((2, ns, 2), dtype=np.int64)
+                if lib.gpr_testing_trd_trace2(tr2.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), ns) == 0:
+                    t2 = tr2[k, :st].astype(np.float64) * 0.01
             for q in range(4):
                 a, b = q * st // 4, (q + 1) * st // 4
                 m = ph[a:b].mean(axis=0)
                 print(f"   steps {a:5d}-{b:5d}: pass {m[0]:6.2f}  publish {m[1]:5.2f}  wait {m[2]:6.2f}  "
                       f"exchange {m[3]:5.2f}  reflector {m[4]:5.2f}  gap {nxt[a:min(b, st - 1)].mean():5.2f}")
+                if t2 is not None and t2[a:b].min() > 0:
+                    c1 = (t2[a:b, 0] - t[a:b, 4]).mean()
+                    c2 = (t2[a:b, 1] - t2[a:b, 0]).mean()
+                    c3 = (t[a:b, 5] - t2[a:b, 1]).mean()
+                    print(f"      (reflector = row chunks {c1:5.2f} + norm, dlarfg {c2:5.2f} + partials {c3:5.2f})")
 
 
 if __name__ == "__main__":

@@ -158,7 +158,6 @@ struct TrdArgs {
   // column j + 1 after step j in rings of 4 columns (ld lda): wr[(j & 3) lda], xr[(j & 3) lda]
   double* wr;
   double* xr;
-  int nt;           // GV pass: non-temporal column loads (bit 0) / stores (bit 1)
   // DF variant (deferred updates, sytrd_df_kernel): w_k in Wv's column k (every workgroup writes
   // the same bits), the panel's dot-product partials in abuf (n x 2 DF_NB x P, each written once),
   // deferred panels for steps j < jt, ncl = ceil(n / P) columns per workgroup
@@ -310,9 +309,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
           const int r = rb + 128 * u;
-          if (r < n)
-            x[u] = (GV && (a.nt & 1)) ? __builtin_nontemporal_load(reinterpret_cast<const d2*>(col + r))
-                                      : *reinterpret_cast<const d2*>(col + r);
+          if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
         }
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
@@ -324,8 +321,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
             if (j > 0) {
               x[u].x -= vp.x * wc + wp.x * vc;
               x[u].y -= vp.y * wc + wp.y * vc;
-              if (GV && (a.nt & 2)) __builtin_nontemporal_store(x[u], reinterpret_cast<d2*>(col + r));
-              else *reinterpret_cast<d2*>(col + r) = x[u];
+              *reinterpret_cast<d2*>(col + r) = x[u];
             }
             if (pub) {
               st1(pub + r, x[u].x);
@@ -1393,10 +1389,6 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   a.abuf = df ? abuf : nullptr;
   a.jt = df ? std::max(0, (n - df_tail) / DF_NB * DF_NB) : 0;
   a.ncl = ncl;
-  a.nt = 0;
-#ifdef GPR_TESTING
-  if (const char* e = getenv("GPR_TRD_NT")) a.nt = atoi(e);  // (A/B)
-#endif
   // cooperative: all P workgroups resident together, or the runtime refuses the launch (nothing
   // has run then: B is untouched, and the caller falls back)
   void* kargs[] = {&a};

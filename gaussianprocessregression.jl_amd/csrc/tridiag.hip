@@ -235,6 +235,70 @@ __device__ bool trd_poll(const TrdArgs& a, int n, int j, int* s_ok, double (&v)[
   }
 }
 
+// trd_poll without pointer arrays (registers): v[k] = base[k * stride] for k < cnt (cnt <= K;
+// the rest inactive)
+template <int K>
+__device__ bool trd_poll_strided(const TrdArgs& a, int n, int j, int* s_ok, double (&v)[K],
+                                 const double* base, int stride, int cnt) {
+  const int tid = threadIdx.x;
+  for (long long spins = 0;; ++spins) {
+    int miss = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) miss |= k < cnt && trd_unset(v[k]);
+    if (!__syncthreads_or(miss)) return true;
+    if ((spins & 63) == 63) {
+      if (tid == 0) {
+        if (spins > a.spin_limit) st1i(a.err, 1);
+        *s_ok = ld1i(a.err) == 0;
+      }
+      __syncthreads();
+      const bool ok = *s_ok != 0;
+      __syncthreads();
+      if (!ok) return false;
+    }
+    if (n - j > 2048) __builtin_amdgcn_s_sleep(31);
+    else __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < cnt && trd_unset(v[k])) v[k] = ld1(base + (size_t)k * stride);
+  }
+}
+
+// the exchange's row chunks: v[2k] = p0[r_k], v[2k+1] = p1[r_k], r_k = rb + k TRD_THREADS
+// (rows >= n inactive)
+template <int G>
+__device__ bool trd_poll_rows(const TrdArgs& a, int n, int j, int* s_ok, double (&v)[2 * G],
+                              const double* p0, const double* p1, int rb) {
+  const int tid = threadIdx.x;
+  for (long long spins = 0;; ++spins) {
+    int miss = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      miss |= rb + k * TRD_THREADS < n && (trd_unset(v[2 * k]) | trd_unset(v[2 * k + 1]));
+    if (!__syncthreads_or(miss)) return true;
+    if ((spins & 63) == 63) {
+      if (tid == 0) {
+        if (spins > a.spin_limit) st1i(a.err, 1);
+        *s_ok = ld1i(a.err) == 0;
+      }
+      __syncthreads();
+      const bool ok = *s_ok != 0;
+      __syncthreads();
+      if (!ok) return false;
+    }
+    if (n - j > 2048) __builtin_amdgcn_s_sleep(31);
+    else __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int r = rb + k * TRD_THREADS;
+      if (r < n) {
+        if (trd_unset(v[2 * k])) v[2 * k] = ld1(p0 + r);
+        if (trd_unset(v[2 * k + 1])) v[2 * k + 1] = ld1(p1 + r);
+      }
+    }
+  }
+}
+
 // Step j's state, identical in every workgroup: vcur = v_j, tau_j; (j > 0) vprev = v_{j-1},
 // wprev = w_{j-1}.  One exchange per step: the pass publishes p_j (and the owner of column
 // j + 1 that column), every workgroup then forms w_j, column j + 1 and v_{j+1} itself.
@@ -649,11 +713,8 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
       const int nct = (ncl - i0 + 15) / 16;  // column tiles of the own columns > j (<= DF_MAXCT)
       const int lr = lane & 15, lg = lane >> 4;
       typedef double d4 __attribute__((ext_vector_type(4)));
-      double dacc[DF_MAXCT][4];
-#pragma unroll
-      for (int ct = 0; ct < DF_MAXCT; ++ct)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dacc[ct][q] = 0.0;
+      for (int i = tid; i < TRD_WAVES * ncl; i += TRD_THREADS) qpart[i] = 0.0;
+      __syncthreads();
       for (int rt = r0 + 16 * wv; rt < n; rt += 16 * TRD_WAVES) {
         const int r = rt + lr;
         const bool rin = r < n;
@@ -693,24 +754,17 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
               a.A[(size_t)c * a.lda + r] = acc[q];
               if (c == j + 1) st1(pubcol + r, acc[q]);
             }
-            dacc[ct][q] += acc[q] * vr;
+            // the tile's part of column i's dot: summed over its 16 rows (lanes l & 15, fixed
+            // order) into the wave's slot (one writer per (wave, column))
+            double sq = acc[q] * vr;
+            sq += __shfl_xor(sq, 1);
+            sq += __shfl_xor(sq, 2);
+            sq += __shfl_xor(sq, 4);
+            sq += __shfl_xor(sq, 8);
+            if (lr == 0 && i < ncl) qpart[wv * ncl + i] += sq;
           }
         }
       }
-      // per column: the sum over this wave's rows (lanes l & 15, fixed order), one writer per
-      // (wave, column)
-#pragma unroll
-      for (int ct = 0; ct < DF_MAXCT; ++ct)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          double sq = dacc[ct][q];
-          sq += __shfl_xor(sq, 1);
-          sq += __shfl_xor(sq, 2);
-          sq += __shfl_xor(sq, 4);
-          sq += __shfl_xor(sq, 8);
-          const int i = i0 + 16 * ct + lg + 4 * q;
-          if (ct < nct && lr == 0 && i < ncl) qpart[wv * ncl + i] = sq;
-        }
       __syncthreads();
       for (int i = i0 + tid; i < ncl; i += TRD_THREADS) {
         const int c = w + i * P;
@@ -841,16 +895,13 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
         TRD_DELAY(5);
         constexpr int AK = DF_MAXP / 16;
         const int q = tid >> 4, sub = tid & 15;
+        // (workgroups sub, sub + 16, ... of value q: cnt of them, none for q >= 2 kk)
+        const int cnt = q < 2 * kk ? (P - sub + 15) / 16 : 0;
+        const double* base = &a.abuf[((size_t)j * 2 * DF_NB + (q < 2 * kk ? q : 0)) * P + sub];
         double v[AK];
-        const double* src[AK];
 #pragma unroll
-        for (int m = 0; m < AK; ++m) {
-          const int ww = sub + 16 * m;
-          const bool act = q < 2 * kk && ww < P;
-          src[m] = act ? &a.abuf[((size_t)j * 2 * DF_NB + q) * P + ww] : nullptr;
-          v[m] = act ? ld1(src[m]) : 0.0;
-        }
-        if (!trd_poll<AK>(a, n, j, s_ok, v, src)) return;
+        for (int m = 0; m < AK; ++m) v[m] = m < cnt ? ld1(base + 16 * m) : 0.0;
+        if (!trd_poll_strided<AK>(a, n, j, s_ok, v, base, 16, cnt)) return;
         double sq = 0.0;
 #pragma unroll
         for (int m = 0; m < AK; ++m) sq += v[m];
@@ -944,16 +995,14 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
       const double wc = pv[0] - kj * vcur[j + 1], vc = vcur[j + 1];
       for (int k0 = 0; j + 1 + k0 * TRD_THREADS < n; k0 += TRD_GCH) {  // (uniform bound)
         double xv[2 * TRD_GCH];
-        const double* xs[2 * TRD_GCH];
 #pragma unroll
         for (int k = 0; k < TRD_GCH; ++k) {
           const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
-          xs[2 * k] = r < n ? &pj[r] : nullptr;
-          xs[2 * k + 1] = r < n ? &pubcol[r] : nullptr;
           xv[2 * k] = r < n ? ld1(&pj[r]) : 0.0;
           xv[2 * k + 1] = r < n ? ld1(&pubcol[r]) : 0.0;
         }
-        if (!trd_poll<2 * TRD_GCH>(a, n, j, s_ok, xv, xs)) return;
+        if (!trd_poll_rows<TRD_GCH>(a, n, j, s_ok, xv, pj, pubcol, j + 1 + tid + k0 * TRD_THREADS))
+          return;
 #pragma unroll
         for (int k = 0; k < TRD_GCH; ++k) {
           const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;

@@ -196,9 +196,11 @@ def _tri(d, e):
     return np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 17, 64, 65, 129, 257, 300, 1100])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 17, 64, 65, 129, 257, 300, 1100, 4700])
 def test_sytrd_random_symmetric(n):
-    """Q^T A Q = T and Q^T Q = I to rounding (Q^T from B = I), T's eigenvalues are A's."""
+    """Q^T A Q = T and Q^T Q = I to rounding (Q^T from B = I), T's eigenvalues are A's.
+    (4700: the deferred-update variant, with B = I past the fused width -- the back-transform
+    by reflector blocks over the V it leaves.)"""
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, n))
     A = (X + X.T) / 2

@@ -30,6 +30,12 @@
 // Cost per step: the store-to-load latency of one hand-off plus 2 (n - j) + P sc1 loads per
 // workgroup, and the pass (16 (n - j)^2 / P bytes per workgroup; the work copy stays in the
 // Infinity Cache up to n ~ 4k).
+//
+// Variants by n: up to TRD_DF_MIN the step vectors sit in LDS (sytrd_kernel<.., GV = false>);
+// from TRD_DF_MIN on the updates are deferred by panels of DF_NB steps (sytrd_df_kernel: later
+// columns only read per step and corrected, flushed per panel by an MFMA GEMM -- 8 instead of
+// 16 (n - j)^2 bytes per step); the per-step global-vector variant (GV = true) remains for
+// grids the DF variant does not cover (more than DF_MAXP workgroups or 16 DF_MAXCT columns each).
 #include <algorithm>
 #include <cmath>
 #include <vector>

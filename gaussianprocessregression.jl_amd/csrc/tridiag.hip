@@ -628,12 +628,13 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
   }
 }
 
-// ---- DF: the reduction with deferred updates (n > TRD_MAXN) ------------------------------
+// ---- DF: the reduction with deferred updates (n >= TRD_DF_MIN) ----------------------------
 // The pass above reads AND writes every trailing column every step (16 (n - j)^2 bytes): at n =
 // 8192 that is ~75 % of the launch, at ~4 TB/s.  DF applies the rank-2 updates by panels of
 // DF_NB steps instead (LAPACK's dlatrd idea, inside the same persistent launch):
 //   * step j of a panel [j0, j0 + DF_NB): the columns the panel will publish, (j, j0 + DF_NB], are
-//     kept up to date as before (eager: read, update, write); every later column is only READ,
+//     kept up to date as before (eager: read, update, write -- each by its owner's whole
+//     workgroup, so no owner becomes the step's straggler); every later column is only READ,
 //     A(:, c) . v_j, and corrected by the panel's pending updates
 //        p_j[c] = tau_j (A(:, c) . v_j - sum_k (w_k[c] alpha_k + v_k[c] beta_k)),
 //        alpha_k = v_k . v_j,  beta_k = w_k . v_j  (k = j0 .. j - 1);
@@ -650,11 +651,11 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
 constexpr int DF_NB = 16;      // updates per panel (the flush: 2 DF_NB registers per row)
 constexpr int DF_TAIL = 1024;  // steps at the end with every update applied at once
 constexpr int DF_MAXP = 256;   // workgroups (the partials' poll: 16 per thread)
-constexpr int DF_MAXCT = 4;
+constexpr int DF_MAXCT = 4;    // the flush's column tiles of 16: ncl <= 64 (n <= 16384 at P = 256)
 // DF from here on: faster than the LDS variant from n ~ 4600 (profiles/r06_trd_df_vs_lds.txt:
 // 5120 155.5 vs 166.1 ms, 6144 227.9 vs 259.8; 4096 101.5 vs 94.8, 3072 62.5 vs 43.4 -- below,
 // the work copy stays in the Infinity Cache and the per-step passes are cheap)
-constexpr int TRD_DF_MIN = 4608;    // the flush's column tiles of 16: ncl <= 64 (n <= 16384 at P = 256)
+constexpr int TRD_DF_MIN = 4608;
 
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
   extern __shared__ double lds[];

@@ -155,6 +155,38 @@ def trd_df_small():
     assert np.max(np.abs(np.linalg.eigvalsh(T) - np.linalg.eigvalsh(A))) <= 4 * n * eps * np.linalg.norm(A, 2)
 
 
+def trd_gv_fallback():
+    """The per-step global-vector reduction (sytrd_kernel<.., GV = true>), the fallback above
+    n = 6144 for grids the deferred-update variant does not cover, forced with GPR_TRD_DF=0 at
+    n = 6200 on a known spectrum (A = H3 H2 H1 diag(ev) H1 H2 H3): T's eigenvalues within
+    4 n eps ||A|| of ev, ||Q^T B|| preserved."""
+    import scipy.linalg as sla
+    import gpr_amd as G
+    ctx = G.Context(0)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    n = 6200
+    rng = np.random.default_rng(n)
+    ev = np.sort(rng.standard_normal(n)) * 3.0
+    A = np.diag(ev)
+    for _ in range(3):
+        v = rng.standard_normal(n)
+        v /= np.linalg.norm(v)
+        Av = A @ v
+        A = A - 2.0 * np.outer(v, Av) - 2.0 * np.outer(Av, v) + 4.0 * (v @ Av) * np.outer(v, v)
+    A = (A + A.T) / 2
+    B = rng.standard_normal((n, 3))
+    os.environ["GPR_TRD_DF"] = "0"
+    dA, dB = ctx.colmajor(A), ctx.colmajor(B)
+    dd, de = ctx.empty(n), ctx.empty(n)
+    assert G._lib.lib.gpr_sytrd_apply(ctx.h, P(dA), n, n, P(dB), 3, n, P(dd), P(de)) == 0, \
+        G._lib.lib.gpr_last_error(ctx.h)
+    del os.environ["GPR_TRD_DF"]
+    lam = sla.eigvalsh_tridiagonal(ctx.host(dd)[:n], ctx.host(de)[:n - 1])
+    assert np.max(np.abs(lam - ev)) <= 4 * n * np.finfo(float).eps * np.abs(ev).max()
+    np.testing.assert_allclose(np.linalg.norm(ctx.host(dB)[:n], axis=0), np.linalg.norm(B, axis=0),
+                               rtol=1e-12)
+
+
 def trd_quad_chunks():
     """The quadrature's per-column tridiagonal solves run in launches of at most
     quad_tridiag_chunk(n, ny) columns (scratch bound); GPR_TRD_QCHUNK (test build) forces 7-

@@ -285,6 +285,14 @@ def test_sytrd_deferred_updates_small_n():
     run_fault_scenario("trd_df_small", timeout=600)
 
 
+def test_sytrd_global_vector_fallback():
+    """The per-step global-vector reduction, kept for grids the deferred-update variant does not
+    cover, forced in the test build at n = 6200 on a known spectrum
+    (tests/fault_scenarios.py trd_gv_fallback)."""
+    from conftest import run_fault_scenario
+    run_fault_scenario("trd_gv_fallback", timeout=600)
+
+
 @pytest.mark.parametrize("n", [4100, 6144, 8192, 8200, 16384])
 def test_syev_large_known_spectrum(n):
     """Large sizes with a known spectrum: n = 4100, the LDS variant's reduction; 6144 and up its

@@ -285,6 +285,26 @@ def test_sytrd_deferred_updates_small_n():
     run_fault_scenario("trd_df_small", timeout=600)
 
 
+@pytest.mark.parametrize("n", [3000, 4700])
+def test_sytrd_fused_vs_blocked_back_transform(n):
+    """Q^T B two ways from the same reduction: B of 1000 columns is transformed inside the
+    launch (at P = 256 workgroups: four columns per workgroup, one wave each), B of 1100 columns
+    afterwards by 64-reflector blocks on the MFMA GEMM.  The same d and e bit for bit, and the
+    first 1000 columns of Q^T B agree to rounding (LDS variant at 3000, deferred-update at
+    4700)."""
+    rng = np.random.default_rng(n + 1)
+    X = rng.standard_normal((n, n))
+    A = (X + X.T) / 2
+    B = rng.standard_normal((n, 1100))
+    ctx = G.Context(0)
+    d1, e1, C1 = _sytrd(ctx, A, B[:, :1000])
+    d2, e2, C2 = _sytrd(ctx, A, B)
+    assert np.array_equal(d1, d2) and np.array_equal(e1, e2)
+    scale = np.linalg.norm(B[:, :1000], axis=0)
+    assert np.max(np.abs(C1 - C2[:, :1000]) / scale) <= 50 * np.sqrt(n) * np.finfo(float).eps
+    np.testing.assert_allclose(np.linalg.norm(C2, axis=0), np.linalg.norm(B, axis=0), rtol=1e-12)
+
+
 def test_sytrd_global_vector_fallback():
     """The per-step global-vector reduction, kept for grids the deferred-update variant does not
     cover, forced in the test build at n = 6200 on a known spectrum

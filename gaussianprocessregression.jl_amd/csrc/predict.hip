@@ -1240,8 +1240,9 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   //      only, PosDefException otherwise); 2 rocSOLVER dsyevd (timing comparator).
   // Unset (-1): per-column factorisations while they cost less than the reduction, else 1 --
   // the crossover from the measured costs (profiles/r05_eig_speed_full.txt: batched ~0.5 + ny (4.3e-12
-  // n^3 + 1.4e-8 n^2) ms, reduction + solves ~0.0061 n + 1.07e-9 n^3 + ny 2e-9 n^2 ms: ny ~ 200 at
-  // n = 4096, ~240 at 2048, ~380 at 1100, ~770 at 512; from n = 4608 on the reduction's
+  // n^3 + 1.4e-8 n^2) ms; reduction + solves ~0.00537 n + 9.3e-10 n^3 + ny 2e-9 n^2 ms below n =
+  // 5376 (profiles/r06_trd_probe_lds_wg.txt: 19.0 / 86.0 / 150 ms at 2048 / 4096 / 5120): ny ~ 175
+  // at n = 4096, ~220 at 2048, ~330 at 1100, ~700 at 512; from n = 5376 on the reduction's
   // deferred-update variant, 3.2e-6 n^2 + 4.6e-10 n^3 -- profiles/r06_trd_probe_df.txt: 467 ms at
   // n = 8192, 1336 at 12288, 228 at 6144, against the batch's 3.3 / 10 ms per column at 8192 /
   // 12288: ny ~ 140); a batch that meets a K + s I that is not
@@ -1251,8 +1252,8 @@ int gpr_integrate_noise(gpr_ctx_t ctx, const int* kinds, int nk, const double* h
   bool fallback = false;
   if (qmode < 0) {
     const double dn = n, t_fac = 0.5 + ny * (4.26e-12 * dn * dn * dn + 1.37e-8 * dn * dn);
-    const double t_red = n >= 4608 ? 3.2e-6 * dn * dn + 4.6e-10 * dn * dn * dn
-                                   : 0.0061 * dn + 1.07e-9 * dn * dn * dn;
+    const double t_red = n >= 5376 ? 3.2e-6 * dn * dn + 4.6e-10 * dn * dn * dn
+                                   : 0.00537 * dn + 9.3e-10 * dn * dn * dn;
     const double t_trd = t_red + ny * 2e-9 * dn * dn;
     qmode = (sym_tridiag_ok(n) && t_trd < t_fac) ? 1 : 0;
     fallback = qmode == 0;

@@ -368,11 +368,50 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     TRD_WGSTAMP(0);
     double sp = 0.0;
     const int r0 = (j + 1) & ~1;
-    const int c0 = w + ((j + 1 - w + P - 1) / P) * P;  // first owned column > j
+    int c0 = w + ((j + 1 - w + P - 1) / P) * P;  // first owned column > j
+    if (c0 == j + 1) {
+      // column j + 1 (its owner): the whole workgroup, rows split over the threads -- updated,
+      // written, published, dotted -- before the other columns (one wave on it, with its
+      // publishing stores, made this workgroup the step's straggler: 49.6 against a median
+      // 37.6 us at n = 4096, profiles/r06_trd_wg_lds_4096.txt)
+      double* col = a.A + (size_t)c0 * a.lda;
+      double* pub = a.cpub + (size_t)(j + 1) * a.lda;
+      const double wc = j > 0 ? wprev[c0] : 0.0, vc = j > 0 ? vprev[c0] : 0.0;
+      double dot = 0.0;
+      for (int rb = r0 + 2 * tid; rb < n; rb += 8 * TRD_THREADS) {
+        d2 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rb + 2 * TRD_THREADS * u;
+          if (r < n) x[u] = *reinterpret_cast<const d2*>(col + r);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rb + 2 * TRD_THREADS * u;
+          if (r < n) {
+            const d2 vv = *reinterpret_cast<const d2*>(vcur + r);
+            if (j > 0) {
+              const d2 vp = *reinterpret_cast<const d2*>(vprev + r);
+              const d2 wp = *reinterpret_cast<const d2*>(wprev + r);
+              x[u].x -= vp.x * wc + wp.x * vc;
+              x[u].y -= vp.y * wc + wp.y * vc;
+              *reinterpret_cast<d2*>(col + r) = x[u];
+            }
+            st1(pub + r, x[u].x);
+            st1(pub + r + 1, x[u].y);
+            dot += (r >= j + 1 ? x[u].x * vv.x : 0.0) + (r + 1 < n ? x[u].y * vv.y : 0.0);
+          }
+        }
+      }
+      const double p = tj * block_sum(dot, red);
+      if (tid == 0) st1(&a.pbuf[(size_t)j * a.lda + c0], p);
+      if (wv == 0) sp += p * vcur[c0];
+      c0 += P;
+    }
     for (int c = c0 + wv * P; c < n; c += TRD_WAVES * P) {
       double* col = a.A + (size_t)c * a.lda;
       const double wc = j > 0 ? wprev[c] : 0.0, vc = j > 0 ? vprev[c] : 0.0;
-      double* pub = c == j + 1 ? a.cpub + (size_t)(j + 1) * a.lda : nullptr;
+      double* pub = nullptr;  // (column j + 1: above)
       double dot = 0.0;
       for (int rb = r0 + 2 * lane; rb < n; rb += PU * 128) {
         d2 x[PU];
@@ -652,10 +691,11 @@ constexpr int DF_NB = 16;      // updates per panel (the flush: 2 DF_NB register
 constexpr int DF_TAIL = 1024;  // steps at the end with every update applied at once
 constexpr int DF_MAXP = 256;   // workgroups (the partials' poll: 16 per thread)
 constexpr int DF_MAXCT = 4;    // the flush's column tiles of 16: ncl <= 64 (n <= 16384 at P = 256)
-// DF from here on: faster than the LDS variant from n ~ 4600 (profiles/r06_trd_df_vs_lds.txt:
-// 5120 155.5 vs 166.1 ms, 6144 227.9 vs 259.8; 4096 101.5 vs 94.8, 3072 62.5 vs 43.4 -- below,
-// the work copy stays in the Infinity Cache and the per-step passes are cheap)
-constexpr int TRD_DF_MIN = 4608;
+// DF from here on: faster than the LDS variant from n ~ 5400 (profiles/r06_trd_df_vs_lds.txt,
+// with the LDS variant's column j + 1 by the whole workgroup: 5632 186.3 vs 190.5 ms, 6144 224.5
+// vs 240.8; 5120 153.6 vs 150.0, 4608 124.9 vs 116.0 -- below, the work copy stays in the
+// Infinity Cache and the per-step passes are cheap)
+constexpr int TRD_DF_MIN = 5376;
 
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
   extern __shared__ double lds[];

@@ -285,7 +285,7 @@ int gpr_cv_batch(gpr_ctx_t ctx, const int* kinds, int nk, const double* hp, int 
  *    never info > 0 (an indefinite K + noise_j I gives the reference's indefinite solve);
  *  - the K + noise_j I factored per column, all in one batched tile-DAG launch that also solves
  *    U_j^{-T} [y_j | k1] (same result within rounding), while that is measured to cost less
- *    (ny below ~200 at n = 4096, ~240 at 2048, ~380 at 1100, ~770 at 512, ~140 at 8192;
+ *    (ny below ~175 at n = 4096, ~220 at 2048, ~330 at 1100, ~700 at 512, ~140 at 8192;
  *    always beyond the reduction's bound n > 16384); a factorisation that fails (a shift at or
  *    below -lambda_min(K)) hands the call to the reduction, so the default never returns
  *    info > 0 up to that bound.  A reduction whose cooperative launch the runtime refuses (its
@@ -318,8 +318,8 @@ int gpr_syev_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, 
  * <- Q^T dB.  One persistent launch (the unblocked two-sided Householder reduction, columns
  * dealt round-robin over the CUs; for m <= 1024 Q^T B is formed inside it), else the
  * back-transform by 64-reflector blocks on the MFMA GEMM.  The launch is cooperative (every
- * workgroup resident or refused up front: GPR_E_UNSUP, nothing touched); below n = 4608 its
- * step vectors sit in LDS and every step updates every trailing column; from 4608 on the
+ * workgroup resident or refused up front: GPR_E_UNSUP, nothing touched); below n = 5376 its
+ * step vectors sit in LDS and every step updates every trailing column; from 5376 on the
  * updates are deferred by panels of 16 steps (later columns only read per step, flushed per
  * panel by an MFMA GEMM).  n <= 16384 (GPR_E_UNSUP beyond). */
 int gpr_sytrd_apply(gpr_ctx_t ctx, const double* dA, int n, int lda, double* dB, int m, int ldb,

@@ -196,10 +196,10 @@ def _tri(d, e):
     return np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 17, 64, 65, 129, 257, 300, 1100, 4700])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 17, 64, 65, 129, 257, 300, 1100, 5500])
 def test_sytrd_random_symmetric(n):
     """Q^T A Q = T and Q^T Q = I to rounding (Q^T from B = I), T's eigenvalues are A's.
-    (4700: the deferred-update variant, with B = I past the fused width -- the back-transform
+    (5500: the deferred-update variant, with B = I past the fused width -- the back-transform
     by reflector blocks over the V it leaves.)"""
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, n))
@@ -277,7 +277,7 @@ def test_sytrd_handoff_timeout_drains_and_context_recovers():
 
 
 def test_sytrd_deferred_updates_small_n():
-    """The deferred-update reduction (n >= 4608 by default) forced at n = 100 .. 4100 in the test
+    """The deferred-update reduction (n >= 5376 by default) forced at n = 100 .. 4100 in the test
     build, with every panel but the last 64 steps deferred: eigenvalues, Q^T B norms and a
     shifted quadratic form against numpy, once under late-wave injection, and a hand-off
     time-out inside a deferred panel (tests/fault_scenarios.py trd_df_small)."""
@@ -285,13 +285,13 @@ def test_sytrd_deferred_updates_small_n():
     run_fault_scenario("trd_df_small", timeout=600)
 
 
-@pytest.mark.parametrize("n", [3000, 4700])
+@pytest.mark.parametrize("n", [3000, 5500])
 def test_sytrd_fused_vs_blocked_back_transform(n):
     """Q^T B two ways from the same reduction: B of 1000 columns is transformed inside the
     launch (at P = 256 workgroups: four columns per workgroup, one wave each), B of 1100 columns
     afterwards by 64-reflector blocks on the MFMA GEMM.  The same d and e bit for bit, and the
     first 1000 columns of Q^T B agree to rounding (LDS variant at 3000, deferred-update at
-    4700)."""
+    5500)."""
     rng = np.random.default_rng(n + 1)
     X = rng.standard_normal((n, n))
     A = (X + X.T) / 2

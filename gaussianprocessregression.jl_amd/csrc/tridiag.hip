@@ -696,6 +696,7 @@ constexpr int DF_MAXCT = 4;    // the flush's column tiles of 16: ncl <= 64 (n <
 // vs 240.8; 5120 153.6 vs 150.0, 4608 124.9 vs 116.0 -- below, the work copy stays in the
 // Infinity Cache and the per-step passes are cheap)
 constexpr int TRD_DF_MIN = 5376;
+constexpr int DF_GCH = 8;  // DF exchange: rows per thread per chunk
 
 __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
   extern __shared__ double lds[];
@@ -1040,18 +1041,18 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
       const double kj = 0.5 * tj * block_sum(pv[1], red);
       TRD_STAMP(4);
       const double wc = pv[0] - kj * vcur[j + 1], vc = vcur[j + 1];
-      for (int k0 = 0; j + 1 + k0 * TRD_THREADS < n; k0 += TRD_GCH) {  // (uniform bound)
-        double xv[2 * TRD_GCH];
+      for (int k0 = 0; j + 1 + k0 * TRD_THREADS < n; k0 += DF_GCH) {  // (uniform bound)
+        double xv[2 * DF_GCH];
 #pragma unroll
-        for (int k = 0; k < TRD_GCH; ++k) {
+        for (int k = 0; k < DF_GCH; ++k) {
           const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
           xv[2 * k] = r < n ? ld1(&pj[r]) : 0.0;
           xv[2 * k + 1] = r < n ? ld1(&pubcol[r]) : 0.0;
         }
-        if (!trd_poll_rows<TRD_GCH>(a, n, j, s_ok, xv, pj, pubcol, j + 1 + tid + k0 * TRD_THREADS))
+        if (!trd_poll_rows<DF_GCH>(a, n, j, s_ok, xv, pj, pubcol, j + 1 + tid + k0 * TRD_THREADS))
           return;
 #pragma unroll
-        for (int k = 0; k < TRD_GCH; ++k) {
+        for (int k = 0; k < DF_GCH; ++k) {
           const int r = j + 1 + tid + (k0 + k) * TRD_THREADS;
           if (r < n) {
             const double wr = xv[2 * k] - kj * vcur[r];

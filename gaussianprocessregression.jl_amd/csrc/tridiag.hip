@@ -108,6 +108,16 @@ __device__ __forceinline__ double wave_sum(double v) {
 __device__ long long g_trd_trace[2][TRD_MAXN][6];
 // every workgroup's pass start / pass end at every 64th step (the spread across workgroups)
 __device__ long long g_trd_wg[TRD_MAXN / 64][256][2];
+// every workgroup's XCD (HW_REG_XCC_ID), recorded at the first step
+__device__ int g_trd_xcc[256];
+#define TRD_XCCSTAMP()                                                          \
+  do {                                                                          \
+    if (tid == 0 && j == 0 && w < 256) {                                        \
+      int x_;                                                                   \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x_));   \
+      g_trd_xcc[w] = x_;                                                        \
+    }                                                                           \
+  } while (0)
 #define TRD_WGSTAMP(k)                                                                      \
   do {                                                                                      \
     if (tid == 0 && j >= a.wgoff && ((j - a.wgoff) & 63) == 0 && w < 256 && j < TRD_MAXN)  \
@@ -134,6 +144,9 @@ __device__ long long g_trd_trace2[2][TRD_MAXN][2];
   } while (0)
 #define TRD_STAMP2(k) \
   do {                \
+  } while (0)
+#define TRD_XCCSTAMP() \
+  do {                 \
   } while (0)
 #endif
 
@@ -366,6 +379,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_kernel(TrdArgs a) {
     // in flight per lane
     TRD_STAMP(0);
     TRD_WGSTAMP(0);
+    TRD_XCCSTAMP();
     double sp = 0.0;
     const int r0 = (j + 1) & ~1;
     int c0 = w + ((j + 1 - w + P - 1) / P) * P;  // first owned column > j
@@ -748,6 +762,7 @@ __global__ __launch_bounds__(TRD_THREADS, 1) void sytrd_df_kernel(TrdArgs a) {
     double sp = 0.0;  // this thread's share of p_j . v_j
     TRD_STAMP(0);
     TRD_WGSTAMP(0);
+    TRD_XCCSTAMP();
     if (j == j0 && j > 0) {
       // ---- flush: the previous panel's DF_NB updates on every own column c > j, then . v_j.
       // A GEMM, X(rows, own columns) -= [V W](rows, 2 DF_NB) [w_k[c]; v_k[c]](2 DF_NB, columns),
@@ -1374,7 +1389,10 @@ int sym_tridiag(gpr_ctx* ctx, const double* dA, int n, int lda, double* dB, int 
   if (const char* e = getenv("GPR_TRD_DF")) df_mode = atoi(e);
   if (const char* e = getenv("GPR_TRD_DF_TAIL")) df_tail = std::max(2 * DF_NB, atoi(e));
 #endif
-  const size_t ld = (size_t)(n + 15) / 16 * 16;
+  size_t ld = (size_t)(n + 15) / 16 * 16;
+#ifdef GPR_TESTING
+  if (const char* e = getenv("GPR_TRD_LDPAD")) ld += (size_t)std::max(0, atoi(e)) / 16 * 16;  // (A/B)
+#endif
   // workgroups: 8 columns each up to n ~ 1500, 16 above (profiles/r05_trd_sweep.txt: 4..24
   // columns change n = 512 / 1100 / 2048 / 4096 by <= 12 / 13 / 11 / 1 %), at most one per CU.
   // (Measured and removed:
@@ -1574,6 +1592,10 @@ extern "C" int gpr_testing_trd_wg_trace(long long* out) {
       hipSuccess)
     return GPR_E_HIP;
   return 0;
+}
+
+extern "C" int gpr_testing_trd_xcc(int* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trd_xcc), sizeof(int) * 256) == hipSuccess ? 0 : GPR_E_HIP;
 }
 
 extern "C" int gpr_testing_trd_trace2(long long* out, int n) {

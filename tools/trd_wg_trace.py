@@ -30,6 +30,11 @@ def main():
     tr = np.zeros((6144 // 64, 256, 2), dtype=np.int64)
     assert lib.gpr_testing_trd_wg_trace(tr.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong))) == 0
     nwg = min(256, (n + 15) // 16) if n > 1536 else min(256, (n + 7) // 8)
+    xcc = np.zeros(256, dtype=np.int32)
+    have_xcc = hasattr(lib, "gpr_testing_trd_xcc") and \
+        lib.gpr_testing_trd_xcc(xcc.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == 0
+    if have_xcc:
+        print("XCC of workgroups 0..15:", " ".join(str(v) for v in xcc[:16]), flush=True)
     for s in range(0, min((n - 2) // 64, 6144 // 64)):  # (steps stamped: below TRD_MAXN)
         st = tr[s, :nwg].astype(np.float64) * 0.01  # us
         dur = st[:, 1] - st[:, 0]
@@ -40,6 +45,10 @@ def main():
             print(f"step {64 * s:5d}: pass {dur.mean():6.2f} us (min {dur.min():6.2f} max {dur.max():6.2f}); "
                   f"start spread {start.max():5.2f}; end spread {end.max():6.2f} us; "
                   f"mean end by XCD " + " ".join(f"{v:5.2f}" for v in byx), flush=True)
+            if have_xcc:
+                byid = [end[:nwg][xcc[:nwg] == x].mean() if (xcc[:nwg] == x).any() else float("nan")
+                        for x in range(8)]
+                print("      mean end by XCC_ID " + " ".join(f"{v:5.2f}" for v in byid), flush=True)
             slow = np.argsort(-dur)[:6]
             print("      slowest: " + " ".join(f"w{w}:{dur[w]:.1f}" for w in slow) +
                   f"  (median {np.median(dur):.1f})", flush=True)
